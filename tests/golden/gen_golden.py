@@ -1,0 +1,134 @@
+#!/usr/bin/env python3
+"""Generate the committed golden fixtures from the COMPILED REFERENCE (oracle/_ref, built from the
+unmodified /root/reference/src/OFDM.c) and from the reference's own data files.
+
+Run in the build container (the GPU box has no /root/reference):
+    python tests/golden/gen_golden.py [--mc-trials 10000]
+
+Outputs (all plain data, loadable with numpy allow_pickle=False / json):
+  fft_vectors.npz      200 random 64-pt inputs and the reference's fft()/ifft() outputs (OFDM.c:314-339)
+  tx_waveform.npz      Transmitter() output (9800 cf32), Data bits, Data_Payload_Mod, Long_preamble_slot_Frequency,
+                       RRC taps (OFDM.c:20-34, 467-618)
+  rx_stages.npz        Receiver() intermediates for injected-noise captures (OFDM.c:941-1165)
+  matlab_output.npz    the 96 KAT bits of data/Matlab_Output.txt (MATLAB Tester RX_Payload_1_demod)
+  reference_data.json  the four data/Output_*.txt files of the reference run (format fixtures)
+  ref_mc_curve.json    Monte-Carlo BER/EVM of the reference's own trial loop (TOA+Receiver) per SNR
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import multiprocessing as mp
+import sys
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+ROOT = HERE.parent.parent
+sys.path.insert(0, str(ROOT))
+from oracle import RefLib, build_ref  # noqa: E402
+
+REF_DATA = Path("/root/reference/data")
+
+
+def gen_fft(R: RefLib):
+    rng = np.random.default_rng(802111)
+    x = (rng.standard_normal((200, 64)) + 1j * rng.standard_normal((200, 64))).astype(np.complex64)
+    # include structured vectors: impulses, constants, OFDM-like sparse spectra
+    x[0] = 0; x[0, 0] = 1
+    x[1] = 0; x[1, 17] = 1 - 2j
+    x[2] = 1
+    f = np.stack([R.fft(v) for v in x])
+    i = np.stack([R.ifft(v) for v in x])
+    np.savez_compressed(HERE / "fft_vectors.npz", x=x, fft=f, ifft=i)
+
+
+def gen_tx(R: RefLib):
+    g = R.globals()
+    np.savez_compressed(HERE / "tx_waveform.npz", waveform=R.waveform(), bits=g["bits"],
+                        payload_mod=g["payload_mod"], ltf_freq=g["ltf_freq"], dims=g["dims"],
+                        rrc_taps=R.rrc_taps())
+
+
+def gen_rx(R: RefLib):
+    w = R.waveform()
+    P = float(np.mean(np.abs(w.astype(np.complex128)) ** 2))
+    cases = [(30.0, 0, 11), (20.0, 1234, 12), (14.0, 777, 13), (10.0, 3000, 14), (8.0, 50, 15),
+             (6.0, 6000, 16), (12.0, 4321, 17), (100.0, 0, 18)]
+    out = {"snr": [], "rx_start": [], "noise": [], "packet_idx": [], "corr": [], "rxframe": [],
+           "coarse": [], "fine": [], "H": [], "Yf": [], "nopilot": [], "bits": [], "res": [], "res_receiver": []}
+    for snr, rs, seed in cases:
+        rng = np.random.default_rng(seed)
+        sigma = np.sqrt(P / 10 ** (snr / 10))
+        # injected real-only noise (D7) on the captured window only
+        noise = np.zeros(len(w), np.float32)
+        noise[rs:rs + 3008] = (sigma * rng.standard_normal(3008)).astype(np.float32)
+        ota = (w + noise).astype(np.complex64)
+        d = R.receiver_stages(ota, rs)
+        rr = R.receiver(ota, rs)
+        assert np.array_equal(np.nan_to_num(rr, neginf=-999), np.nan_to_num(d["res"], neginf=-999)), (rr, d["res"])
+        out["snr"].append(snr); out["rx_start"].append(rs); out["noise"].append(noise[rs:rs + 3008])
+        out["packet_idx"].append(d["packet_idx"]); out["res_receiver"].append(rr)
+        for k in ("corr", "rxframe", "coarse", "fine", "H", "Yf", "nopilot", "bits", "res"):
+            out[k].append(d[k])
+    np.savez_compressed(HERE / "rx_stages.npz", **{k: np.array(v) for k, v in out.items()})
+
+
+def gen_kat():
+    kat = np.array([int(float(t)) for t in (REF_DATA / "Matlab_Output.txt").read_text().split()], np.int32)
+    np.savez_compressed(HERE / "matlab_output.npz", bits=kat)
+    files = {n: (REF_DATA / n).read_text() for n in
+             ("Output_SNR.txt", "Output_EVM_AGC.txt", "Output_EVM_AGC_DB.txt", "Output_BER.txt")}
+    (HERE / "reference_data.json").write_text(json.dumps(files, indent=1))
+
+
+def _mc_worker(args):
+    snr, n, seed = args
+    R = RefLib()
+    t, acc = R.time_trials(snr, n, seed)
+    return snr, n, t, acc.tolist()
+
+
+def gen_mc(trials: int, procs: int):
+    snrs = list(range(0, 17)) + [18, 20, 22, 24, 26, 28, 30]
+    jobs = []
+    per = max(1, trials // procs)
+    for s in snrs:
+        for p in range(procs):
+            jobs.append((float(s), per, 1000003 * (p + 1) + int(s)))
+    with mp.Pool(procs) as pool:
+        res = pool.map(_mc_worker, jobs)
+    curve = {}
+    for snr, n, t, acc in res:
+        c = curve.setdefault(snr, {"trials": 0, "sum_evm_db": 0.0, "sum_evm_agc_db": 0.0, "sum_ber": 0.0, "sec": 0.0})
+        c["trials"] += n; c["sum_evm_db"] += acc[0]; c["sum_evm_agc_db"] += acc[1]; c["sum_ber"] += acc[2]
+        c["sec"] += t
+    rows = []
+    for snr in sorted(curve):
+        c = curve[snr]
+        rows.append({"snr_db": snr, "trials": c["trials"], "ber": c["sum_ber"] / c["trials"],
+                     "mean_evm_db": c["sum_evm_db"] / c["trials"],
+                     "mean_evm_agc_db": c["sum_evm_agc_db"] / c["trials"],
+                     "sec_per_trial": c["sec"] / c["trials"]})
+    meta = {"generator": "tests/golden/gen_golden.py", "source": "reference OFDM.c (gcc -O2) TOA+Receiver loop",
+            "rand": "64-bit LCG hook (oracle/ref_harness.c)", "rows": rows}
+    (HERE / "ref_mc_curve.json").write_text(json.dumps(meta, indent=1))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mc-trials", type=int, default=8000)
+    ap.add_argument("--procs", type=int, default=8)
+    ap.add_argument("--skip-mc", action="store_true")
+    a = ap.parse_args()
+    build_ref()
+    R = RefLib()
+    gen_fft(R); gen_tx(R); gen_rx(R); gen_kat()
+    if not a.skip_mc:
+        gen_mc(a.mc_trials, a.procs)
+    print("golden fixtures written to", HERE)
+
+
+if __name__ == "__main__":
+    main()
