@@ -1,0 +1,120 @@
+"""ctypes binding of the C ABI in include/ofdm_mi355x.h (libofdm_mi355x.so).
+
+The library is the product: there is no CPU or PyTorch fallback.  If the shared object is
+missing or cannot be loaded, load_library() raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+PKG_DIR = Path(__file__).resolve().parent
+LIB_PATH = PKG_DIR / "libofdm_mi355x.so"
+HEADER = PKG_DIR.parent / "include" / "ofdm_mi355x.h"
+
+ABI_VERSION = 1
+
+# enums (include/ofdm_mi355x.h)
+CONV = {"c": 0, "matlab": 1}
+PAYLOAD = {"random": 0, "message": 1, "tester": 2}
+EST = {"ls": 0, "ideal": 1}
+NOISE = {"real": 0, "complex": 1, "none": 2}
+CHANNEL = {"awgn": 0, "rayleigh4": 1}
+
+# counters
+NCOUNTERS = 16
+C_FRAMES, C_SYMBOLS, C_BITS, C_BIT_ERR, C_FRAME_ERR, C_SYNC_FAIL, C_EVM_TERMS, C_EVM_PRE_Q, \
+    C_EVM_POST_AXIS, C_EVMDB_PRE_Q, C_EVMDB_POST_Q, C_EVMDB_POST_FINITE, C_OOB = range(13)
+EVM_Q_SCALE = float(1 << 20)
+
+# kernel ids for timing
+K_FFT, K_TX, K_RX, K_FRAME = range(4)
+
+# every entry point of the header, with ctypes argument types
+_V = C.c_void_p
+_SIGS = {
+    "ofdm_abi_version": (C.c_int, []),
+    "ofdm_last_error": (C.c_char_p, []),
+    "ofdm_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "ofdm_ctx_create": (C.c_int, [C.c_int, C.POINTER(_V)]),
+    "ofdm_ctx_destroy": (C.c_int, [_V]),
+    "ofdm_ctx_set_stream": (C.c_int, [_V, _V]),
+    "ofdm_ctx_synchronize": (C.c_int, [_V]),
+    "ofdm_timing_enable": (C.c_int, [_V, C.c_int]),
+    "ofdm_timing_query": (C.c_int, [_V, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
+    "ofdm_timing_reset": (C.c_int, [_V]),
+    "ofdm_fft64": (C.c_int, [_V, _V, _V, C.c_int64, C.c_int, C.c_int]),
+    "ofdm_tx_bytes": (C.c_int, [C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+    "ofdm_tx_frames": (C.c_int, [_V, _V, C.c_uint64, C.c_int64, _V, _V]),
+    "ofdm_rx_frames": (C.c_int, [_V, _V, _V, _V, C.c_uint64, C.c_int64, _V, C.c_int, _V]),
+    "ofdm_rx_frames_dump": (C.c_int, [_V, _V, _V, _V, C.c_uint64, C.c_int64, _V, C.c_int, _V, _V, _V]),
+    "ofdm_symbol_sweep": (C.c_int, [_V, _V, _V, C.c_int, C.c_uint64, C.c_int64, C.c_int64, _V]),
+    "ofdm_transmitter": (C.c_int, [_V, C.c_int, C.c_int, C.c_int, _V, C.c_int32, C.POINTER(C.c_int32)]),
+    "ofdm_transmission_over_air": (C.c_int, [_V, _V, _V, C.c_int32, C.c_double, C.c_uint64, C.c_uint64, C.c_int32]),
+    "ofdm_receiver": (C.c_int, [_V, _V, _V, C.c_int, _V, _V, _V, _V]),
+    "ofdm_frame_sweep": (C.c_int, [_V, _V, _V, _V, C.c_int, C.c_uint64, C.c_int64, _V, _V]),
+}
+EXPORTS = tuple(_SIGS)
+
+
+class OfdmError(RuntimeError):
+    pass
+
+
+class Cfg(C.Structure):
+    """ofdm_cfg"""
+    _fields_ = [("seed", C.c_uint64), ("conv", C.c_int32), ("payload", C.c_int32), ("est", C.c_int32),
+                ("noise", C.c_int32), ("channel", C.c_int32), ("data_per_frame", C.c_int32),
+                ("kappa", C.c_double), ("p_ref", C.c_double)]
+
+
+class RxOpts(C.Structure):
+    """ofdm_rx_opts"""
+    _fields_ = [("cap_len", C.c_int32), ("float_cfo", C.c_int32), ("matlab_slicer", C.c_int32),
+                ("float_taps", C.c_int32), ("fixed_start", C.c_int32), ("reserved", C.c_int32 * 3)]
+
+
+def make_cfg(seed: int = 0x80211A, conv: str = "c", payload: str = "random", est: str = "ls",
+             noise: str = "real", channel: str = "awgn", kappa: float = 0.4980,
+             p_ref: float = 52.0 / 4096.0) -> Cfg:
+    return Cfg(seed, CONV[conv], PAYLOAD[payload], EST[est], NOISE[noise], CHANNEL[channel], 2, kappa, p_ref)
+
+
+def make_rx_opts(mode: str = "c", fixed_start: int = -1) -> RxOpts:
+    """mode 'c': OFDM.c receiver (capture 3008 = floor(0.307*9800), fp32 CFO, fp32 taps);
+    'matlab': IEEE_802_11_a_Code_Tester.m (capture 3000, MATLAB slicer, double taps)."""
+    if mode == "c":
+        return RxOpts(3008, 1, 0, 1, fixed_start)
+    if mode == "matlab":
+        return RxOpts(3000, 0, 1, 0, fixed_start)
+    raise ValueError(mode)
+
+
+_LIB = None
+
+
+def load_library(path: Path | str | None = None) -> C.CDLL:
+    """Load libofdm_mi355x.so (build it first with build_lib.build()).  Raises if absent."""
+    global _LIB
+    if _LIB is not None and path is None:
+        return _LIB
+    p = Path(path or LIB_PATH)
+    if not p.exists():
+        raise OfdmError(f"{p} not found: the HIP library must be built (build_lib.build()); "
+                        "there is no CPU fallback")
+    lib = C.CDLL(str(p))
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.ofdm_abi_version() != ABI_VERSION:
+        raise OfdmError(f"ABI mismatch: library {lib.ofdm_abi_version()} != {ABI_VERSION}")
+    if path is None:
+        _LIB = lib
+    return lib
+
+
+def check(lib: C.CDLL, rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = lib.ofdm_last_error()
+        raise OfdmError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")

@@ -1,0 +1,363 @@
+// ofdm_capi.hip -- the extern "C" boundary (include/ofdm_mi355x.h): contexts, streams, device
+// buffers, kernel timing and the symbol-mode sweep driver.  Host code only (the kernels are in
+// ofdm_symbol.hip / ofdm_frame.hip).
+#include <hip/hip_runtime.h>
+#include <cmath>
+#include <complex>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+#include "ofdm_internal.h"
+#include "ofdm_ctx.h"
+
+using namespace ofdm;
+
+namespace ofdm {
+
+thread_local std::string g_last_error;
+
+int set_error(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+// ------------------------------------------------------------------ host-side frame constants
+// Long training symbol T = ifft(Lf) (Preamble_Generator, OFDM.c:368-399) in double, per
+// convention; Lf = [0 x6, L_k (53), 0 x5] (OFDM.c:494).
+static void host_ltf_time(int conv, std::vector<float2> &out) {
+    std::complex<double> X[64], Xs[64], v[64];
+    for (int i = 0; i < 64; ++i) X[i] = (double)ltf_sign(i);
+    for (int i = 0; i < 64; ++i) Xs[i] = X[(i + 32) & 63];                    // ifftshift
+    const double tp = 6.283185307179586476925286766559;
+    for (int n = 0; n < 64; ++n) {
+        std::complex<double> acc = 0;
+        for (int m = 0; m < 64; ++m) acc += Xs[m] * std::polar(1.0, tp * ((m * n) & 63) / 64.0);
+        v[n] = acc / 64.0;
+    }
+    out.resize(64);
+    for (int n = 0; n < 64; ++n) {
+        const std::complex<double> y = (conv == OFDM_CONV_C) ? v[(n + 32) & 63] : v[n];   // fftshift (C)
+        out[n] = make_float2((float)y.real(), (float)y.imag());
+    }
+}
+
+// payload words: reference message (Data_Generator, OFDM.c:435-465) or MATLAB Tester (Tester.m:50-51)
+void payload_table(int payload, uint32_t table[6]) {
+    unsigned char bytes[24];
+    if (payload == OFDM_PAYLOAD_TESTER) {
+        for (int f = 0; f < 2; ++f)
+            for (int c = 0; c < 12; ++c) bytes[12 * f + c] = c < 11 ? 0x41 : 0x20;
+    } else {
+        static const char msg[] = "Hey! I am Vivaswan";          // OFDM.c:20
+        const int len = (int)sizeof(msg) - 1;
+        for (int c = 0; c < 24; ++c) bytes[c] = c < len ? (unsigned char)msg[c] : ' ';
+    }
+    for (int w = 0; w < 6; ++w)
+        table[w] = ((uint32_t)bytes[4 * w] << 24) | ((uint32_t)bytes[4 * w + 1] << 16) |
+                   ((uint32_t)bytes[4 * w + 2] << 8) | (uint32_t)bytes[4 * w + 3];
+}
+
+int check_cfg(const ofdm_cfg *c) {
+    if (!c) return set_error(OFDM_E_ARG, "cfg is NULL");
+    if (c->conv != OFDM_CONV_C && c->conv != OFDM_CONV_MATLAB) return set_error(OFDM_E_ARG, "bad conv %d", c->conv);
+    if (c->payload < 0 || c->payload > 2) return set_error(OFDM_E_ARG, "bad payload %d", c->payload);
+    if (c->est != OFDM_EST_LS && c->est != OFDM_EST_IDEAL) return set_error(OFDM_E_ARG, "bad est %d", c->est);
+    if (c->noise < 0 || c->noise > 2) return set_error(OFDM_E_ARG, "bad noise %d", c->noise);
+    if (c->channel != OFDM_CHAN_AWGN && c->channel != OFDM_CHAN_RAYLEIGH4)
+        return set_error(OFDM_E_ARG, "bad channel %d", c->channel);
+    if (c->data_per_frame != 2) return set_error(OFDM_E_ARG, "data_per_frame must be 2 (got %d)", c->data_per_frame);
+    if (!(c->kappa > 0) || !(c->p_ref > 0)) return set_error(OFDM_E_ARG, "kappa and p_ref must be > 0");
+    return OFDM_OK;
+}
+
+// ------------------------------------------------------------------ timing
+void Ctx::tic(int k) {
+    if (!timing) return;
+    Ev e;
+    e.kernel = k;
+    if (!pool.empty()) { e.a = pool.back(); pool.pop_back(); } else hipEventCreate(&e.a);
+    if (!pool.empty()) { e.b = pool.back(); pool.pop_back(); } else hipEventCreate(&e.b);
+    hipEventRecord(e.a, stream);
+    open.push_back(e);
+}
+void Ctx::toc() {
+    if (!timing || open.empty()) return;
+    hipEventRecord(open.back().b, stream);
+    done.push_back(open.back());
+    open.pop_back();
+}
+void Ctx::resolve() {
+    for (auto &e : done) {
+        float ms = 0.f;
+        hipEventSynchronize(e.b);
+        hipEventElapsedTime(&ms, e.a, e.b);
+        acc_ms[e.kernel] += ms;
+        launches[e.kernel] += 1;
+        pool.push_back(e.a);
+        pool.push_back(e.b);
+    }
+    done.clear();
+}
+
+int Ctx::ensure(void **p, size_t *cap, size_t bytes) {
+    if (*cap >= bytes) return OFDM_OK;
+    if (*p) hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (hipMalloc(p, bytes) != hipSuccess) {
+        *p = nullptr;
+        return set_error(OFDM_E_NOMEM, "hipMalloc(%zu) failed", bytes);
+    }
+    *cap = bytes;
+    return OFDM_OK;
+}
+
+}  // namespace ofdm
+
+#define HIPOK(expr)                                                                             \
+    do {                                                                                        \
+        hipError_t e_ = (expr);                                                                 \
+        if (e_ != hipSuccess) return set_error(OFDM_E_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+extern "C" {
+
+int ofdm_abi_version(void) { return OFDM_ABI_VERSION; }
+const char *ofdm_last_error(void) { return g_last_error.c_str(); }
+
+int ofdm_device_count(int *count) {
+    if (!count) return set_error(OFDM_E_ARG, "count is NULL");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return OFDM_OK;
+}
+
+int ofdm_ctx_create(int device, ofdm_ctx **out) {
+    if (!out) return set_error(OFDM_E_ARG, "out is NULL");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return set_error(OFDM_E_NODEV, "no HIP device visible");
+    if (device < 0 || device >= n) return set_error(OFDM_E_ARG, "device %d out of range [0,%d)", device, n);
+    HIPOK(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIPOK(hipGetDeviceProperties(&prop, device));
+    if (!strstr(prop.gcnArchName, "gfx950"))
+        return set_error(OFDM_E_NODEV, "device %d is %s; this library is built for gfx950 only", device, prop.gcnArchName);
+    Ctx *c = new Ctx();
+    c->device = device;
+    c->cus = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return set_error(OFDM_E_HIP, "hipStreamCreate failed");
+    }
+    c->stream = c->own;
+    for (int conv = 0; conv < 2; ++conv) {
+        std::vector<float2> t;
+        host_ltf_time(conv, t);
+        if (hipMalloc(&c->d_ltf[conv], 64 * sizeof(float2)) != hipSuccess ||
+            hipMemcpy(c->d_ltf[conv], t.data(), 64 * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess) {
+            ofdm_ctx_destroy(reinterpret_cast<ofdm_ctx *>(c));
+            return set_error(OFDM_E_NOMEM, "LTF table upload failed");
+        }
+    }
+    *out = reinterpret_cast<ofdm_ctx *>(c);
+    return OFDM_OK;
+}
+
+int ofdm_ctx_destroy(ofdm_ctx *ctx) {
+    Ctx *c = reinterpret_cast<Ctx *>(ctx);
+    if (!c) return OFDM_OK;
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    for (auto &e : c->done) { hipEventDestroy(e.a); hipEventDestroy(e.b); }
+    for (auto &e : c->open) { hipEventDestroy(e.a); hipEventDestroy(e.b); }
+    for (auto ev : c->pool) hipEventDestroy(ev);
+    for (void *p : {(void *)c->d_ltf[0], (void *)c->d_ltf[1], c->d_tx, c->d_bits, c->d_cnt, c->d_scratch,
+                    c->d_scratch2, c->d_wave})
+        if (p) hipFree(p);
+    if (c->own) hipStreamDestroy(c->own);
+    delete c;
+    return OFDM_OK;
+}
+
+int ofdm_ctx_set_stream(ofdm_ctx *ctx, void *stream) {
+    Ctx *c = reinterpret_cast<Ctx *>(ctx);
+    if (!c) return set_error(OFDM_E_ARG, "ctx is NULL");
+    c->stream = stream ? reinterpret_cast<hipStream_t>(stream) : c->own;
+    return OFDM_OK;
+}
+
+int ofdm_ctx_synchronize(ofdm_ctx *ctx) {
+    Ctx *c = reinterpret_cast<Ctx *>(ctx);
+    if (!c) return set_error(OFDM_E_ARG, "ctx is NULL");
+    HIPOK(hipSetDevice(c->device));
+    HIPOK(hipStreamSynchronize(c->stream));
+    return OFDM_OK;
+}
+
+int ofdm_timing_enable(ofdm_ctx *ctx, int enable) {
+    Ctx *c = reinterpret_cast<Ctx *>(ctx);
+    if (!c) return set_error(OFDM_E_ARG, "ctx is NULL");
+    c->timing = enable != 0;
+    return OFDM_OK;
+}
+
+int ofdm_timing_query(ofdm_ctx *ctx, int kernel, double *ms_total, int64_t *launches) {
+    Ctx *c = reinterpret_cast<Ctx *>(ctx);
+    if (!c || kernel < 0 || kernel >= Ctx::NK) return set_error(OFDM_E_ARG, "bad ctx/kernel");
+    hipSetDevice(c->device);
+    c->resolve();
+    if (ms_total) *ms_total = c->acc_ms[kernel];
+    if (launches) *launches = c->launches[kernel];
+    return OFDM_OK;
+}
+
+int ofdm_timing_reset(ofdm_ctx *ctx) {
+    Ctx *c = reinterpret_cast<Ctx *>(ctx);
+    if (!c) return set_error(OFDM_E_ARG, "ctx is NULL");
+    hipSetDevice(c->device);
+    c->resolve();
+    for (int k = 0; k < Ctx::NK; ++k) { c->acc_ms[k] = 0; c->launches[k] = 0; }
+    return OFDM_OK;
+}
+
+int ofdm_fft64(ofdm_ctx *ctx, const void *d_in, void *d_out, int64_t n, int inverse, int conv) {
+    Ctx *c = reinterpret_cast<Ctx *>(ctx);
+    if (!c || (!d_in && n) || (!d_out && n) || n < 0) return set_error(OFDM_E_ARG, "bad fft64 arguments");
+    if (conv != OFDM_CONV_C && conv != OFDM_CONV_MATLAB) return set_error(OFDM_E_ARG, "bad conv %d", conv);
+    if (n == 0) return OFDM_OK;
+    HIPOK(hipSetDevice(c->device));
+    c->tic(Ctx::K_FFT);
+    launch_fft64(c->stream, (const float2 *)d_in, (float2 *)d_out, n, inverse, conv);
+    c->toc();
+    HIPOK(hipGetLastError());
+    return OFDM_OK;
+}
+
+int ofdm_tx_bytes(int64_t n_frames, int64_t *tx_bytes, int64_t *bits_bytes) {
+    if (n_frames < 0) return set_error(OFDM_E_ARG, "n_frames < 0");
+    const int64_t t = tiles_for(n_frames);
+    if (tx_bytes) *tx_bytes = t * SYM_SAMPLES * TILE_SYMBOLS * (int64_t)sizeof(float2);
+    if (bits_bytes) *bits_bytes = t * 3 * TILE_SYMBOLS * (int64_t)sizeof(uint32_t);
+    return OFDM_OK;
+}
+
+int ofdm_tx_frames(ofdm_ctx *ctx, const ofdm_cfg *cfg, uint64_t first_frame, int64_t n_frames, void *d_tx,
+                   void *d_bits) {
+    Ctx *c = reinterpret_cast<Ctx *>(ctx);
+    if (!c) return set_error(OFDM_E_ARG, "ctx is NULL");
+    int rc = check_cfg(cfg);
+    if (rc) return rc;
+    if (n_frames < 0 || (n_frames && (!d_tx || !d_bits))) return set_error(OFDM_E_ARG, "bad tx buffers");
+    if (n_frames == 0) return OFDM_OK;
+    HIPOK(hipSetDevice(c->device));
+    TxArgs a{};
+    a.tx = (float2 *)d_tx;
+    a.bits = (uint32_t *)d_bits;
+    a.first_symbol = 2 * first_frame;
+    a.n_sym = tiles_for(n_frames) * TILE_SYMBOLS;
+    a.k0 = (uint32_t)cfg->seed;
+    a.k1 = (uint32_t)(cfg->seed >> 32);
+    a.payload = cfg->payload;
+    payload_table(cfg->payload, a.table);
+    c->tic(Ctx::K_TX);
+    launch_tx(c->stream, a, cfg->conv);
+    c->toc();
+    HIPOK(hipGetLastError());
+    return OFDM_OK;
+}
+
+static int rx_common(Ctx *c, const ofdm_cfg *cfg, const void *d_tx, const void *d_bits, uint64_t first_frame,
+                     int64_t n_frames, const double *snr_db, int n_snr, void *d_counters, void *d_eq, void *d_dbits) {
+    if (!c) return set_error(OFDM_E_ARG, "ctx is NULL");
+    int rc = check_cfg(cfg);
+    if (rc) return rc;
+    if (n_snr < 0 || (n_snr && !snr_db) || !d_counters) return set_error(OFDM_E_ARG, "bad snr/counters");
+    if (n_frames < 0 || (n_frames && (!d_tx || !d_bits))) return set_error(OFDM_E_ARG, "bad rx buffers");
+    if (n_frames == 0 || n_snr == 0) return OFDM_OK;
+    const bool dump = d_eq || d_dbits;
+    if (dump && (!d_eq || !d_dbits)) return set_error(OFDM_E_ARG, "dump needs both d_eq and d_dbits");
+    HIPOK(hipSetDevice(c->device));
+    const int64_t n_tiles = tiles_for(n_frames);
+    const unsigned grid = (unsigned)rx_grid(*cfg, n_tiles, c->device);
+    for (int q0 = 0; q0 < n_snr; q0 += OFDM_MAX_SNR) {
+        RxArgs a{};
+        a.tx = (const float2 *)d_tx;
+        a.bits = (const uint32_t *)d_bits;
+        a.ltf = c->d_ltf[cfg->conv];
+        a.first_frame = first_frame;
+        a.n_frames = n_frames;
+        a.n_tiles = n_tiles;
+        a.k0 = (uint32_t)cfg->seed;
+        a.k1 = (uint32_t)(cfg->seed >> 32);
+        a.n_snr = std::min(OFDM_MAX_SNR, n_snr - q0);
+        a.q_base = q0;
+        a.counters = (unsigned long long *)d_counters + (size_t)q0 * OFDM_NCOUNTERS;
+        a.dump_frames = n_frames;
+        if (dump) {
+            a.dump_eq = (float2 *)d_eq + (size_t)q0 * n_frames * 2 * 48;
+            a.dump_bits = (uint32_t *)d_dbits + (size_t)q0 * n_frames * 2 * 3;
+        }
+        for (int q = 0; q < a.n_snr; ++q) {
+            const double s2 = cfg->kappa * cfg->p_ref / std::pow(10.0, snr_db[q0 + q] / 10.0);
+            a.sigma[q] = (float)std::sqrt(s2);
+        }
+        c->tic(Ctx::K_RX);
+        launch_rx(c->stream, a, *cfg, dump, grid);
+        c->toc();
+        HIPOK(hipGetLastError());
+    }
+    return OFDM_OK;
+}
+
+int ofdm_rx_frames(ofdm_ctx *ctx, const ofdm_cfg *cfg, const void *d_tx, const void *d_bits, uint64_t first_frame,
+                   int64_t n_frames, const double *snr_db, int n_snr, void *d_counters) {
+    return rx_common(reinterpret_cast<Ctx *>(ctx), cfg, d_tx, d_bits, first_frame, n_frames, snr_db, n_snr,
+                     d_counters, nullptr, nullptr);
+}
+
+int ofdm_rx_frames_dump(ofdm_ctx *ctx, const ofdm_cfg *cfg, const void *d_tx, const void *d_bits,
+                        uint64_t first_frame, int64_t n_frames, const double *snr_db, int n_snr, void *d_counters,
+                        void *d_eq, void *d_dbits) {
+    return rx_common(reinterpret_cast<Ctx *>(ctx), cfg, d_tx, d_bits, first_frame, n_frames, snr_db, n_snr,
+                     d_counters, d_eq, d_dbits);
+}
+
+int ofdm_symbol_sweep(ofdm_ctx *ctx, const ofdm_cfg *cfg, const double *snr_db, int n_snr, uint64_t first_frame,
+                      int64_t n_frames, int64_t chunk_frames, int64_t *counters) {
+    Ctx *c = reinterpret_cast<Ctx *>(ctx);
+    if (!c) return set_error(OFDM_E_ARG, "ctx is NULL");
+    int rc = check_cfg(cfg);
+    if (rc) return rc;
+    if (n_snr < 0 || (n_snr && (!snr_db || !counters)) || n_frames < 0) return set_error(OFDM_E_ARG, "bad sweep args");
+    if (n_snr == 0) return OFDM_OK;
+    HIPOK(hipSetDevice(c->device));
+    const size_t cbytes = (size_t)n_snr * OFDM_NCOUNTERS * sizeof(int64_t);
+    if ((rc = c->ensure(&c->d_cnt, &c->cap_cnt, cbytes))) return rc;
+    HIPOK(hipMemsetAsync(c->d_cnt, 0, cbytes, c->stream));
+    if (chunk_frames <= 0) chunk_frames = int64_t(1) << 22;           // 8.4M symbols, ~5.5 GB per chunk
+    chunk_frames = (chunk_frames + TILE_FRAMES - 1) / TILE_FRAMES * TILE_FRAMES;
+    const int64_t cf = std::min<int64_t>(chunk_frames, std::max<int64_t>(n_frames, 1));
+    int64_t txb = 0, bb = 0;
+    ofdm_tx_bytes(cf, &txb, &bb);
+    if ((rc = c->ensure(&c->d_tx, &c->cap_tx, (size_t)txb))) return rc;
+    if ((rc = c->ensure(&c->d_bits, &c->cap_bits, (size_t)bb))) return rc;
+    for (int64_t done = 0; done < n_frames; done += cf) {
+        const int64_t nf = std::min(cf, n_frames - done);
+        if ((rc = ofdm_tx_frames(ctx, cfg, first_frame + done, nf, c->d_tx, c->d_bits))) return rc;
+        if ((rc = ofdm_rx_frames(ctx, cfg, c->d_tx, c->d_bits, first_frame + done, nf, snr_db, n_snr, c->d_cnt))) return rc;
+    }
+    HIPOK(hipMemcpyAsync(counters, c->d_cnt, cbytes, hipMemcpyDeviceToHost, c->stream));
+    HIPOK(hipStreamSynchronize(c->stream));
+    return OFDM_OK;
+}
+
+}  // extern "C"

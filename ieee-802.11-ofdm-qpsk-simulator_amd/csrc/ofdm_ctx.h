@@ -1,0 +1,44 @@
+// ofdm_ctx.h -- the opaque ofdm_ctx behind the C ABI (host-side state of one GPU).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdarg>
+#include <string>
+#include <vector>
+#include "ofdm_mi355x.h"
+
+namespace ofdm {
+
+int set_error(int code, const char *fmt, ...);
+int check_cfg(const ofdm_cfg *c);
+void payload_table(int payload, uint32_t table[6]);
+
+struct Ctx {
+    enum { K_FFT = 0, K_TX = 1, K_RX = 2, K_FRAME = 3, NK = 4 };
+    int device = 0;
+    int cus = 256;
+    hipStream_t own = nullptr;       // created by the context
+    hipStream_t stream = nullptr;    // where work is enqueued (own or external)
+    float2 *d_ltf[2] = {nullptr, nullptr};
+    // sweep scratch (grown on demand, freed with the context)
+    void *d_tx = nullptr, *d_bits = nullptr, *d_cnt = nullptr, *d_scratch = nullptr, *d_scratch2 = nullptr;
+    void *d_wave = nullptr;
+    size_t cap_tx = 0, cap_bits = 0, cap_cnt = 0, cap_scratch = 0, cap_scratch2 = 0, cap_wave = 0;
+    // frame-mode waveform cache (per conv/payload/taps)
+    int wave_key = -1;
+    int32_t wave_len = 0;
+    double wave_power = 0.0;
+    // kernel timing
+    struct Ev { hipEvent_t a, b; int kernel; };
+    bool timing = false;
+    std::vector<Ev> open, done;
+    std::vector<hipEvent_t> pool;
+    double acc_ms[NK] = {0, 0, 0, 0};
+    int64_t launches[NK] = {0, 0, 0, 0};
+
+    void tic(int k);
+    void toc();
+    void resolve();
+    int ensure(void **p, size_t *cap, size_t bytes);
+};
+
+}  // namespace ofdm

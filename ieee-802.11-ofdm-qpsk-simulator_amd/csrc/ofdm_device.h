@@ -1,0 +1,241 @@
+// ofdm_device.h -- device building blocks for the gfx950 OFDM Monte-Carlo kernels.
+//
+//  * Philox4x32-10 counter-based RNG (Salmon et al., SC'11; Random123 constants), keyed by the
+//    64-bit seed; the stream/counter layout is DESIGN.md §3 (shared with oracle/ofdm_oracle.c).
+//  * Box-Muller on the hardware transcendentals (v_log_f32, v_sqrt_f32, v_sin/v_cos_f32 which
+//    take revolutions, so 2*pi*u needs no range reduction).
+//  * a fully unrolled radix-4 decimation-in-frequency 64-point FFT held in one lane's VGPRs
+//    (x[64] indexed only by compile-time constants), digit-reversed output.  One lane owns one
+//    OFDM symbol, so no cross-lane traffic is needed on the hot path.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <type_traits>
+#include "twiddle64.h"
+
+namespace ofdm {
+
+// ------------------------------------------------------------------ compile-time loops
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F &&f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
+
+// ------------------------------------------------------------------ complex helpers
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+    return make_float2(fmaf(a.x, b.x, -a.y * b.y), fmaf(a.x, b.y, a.y * b.x));
+}
+__device__ __forceinline__ float2 cmulc(float2 a, float2 b) {  // a * conj(b)
+    return make_float2(fmaf(a.x, b.x, a.y * b.y), fmaf(a.y, b.x, -a.x * b.y));
+}
+
+// ------------------------------------------------------------------ Philox4x32-10
+constexpr uint32_t PHILOX_M0 = 0xD2511F53u, PHILOX_M1 = 0xCD9E8D57u;
+constexpr uint32_t PHILOX_W0 = 0x9E3779B9u, PHILOX_W1 = 0xBB67AE85u;
+// stream tags in counter word 3
+constexpr uint32_t STREAM_BITS = 0xB1750000u;
+constexpr uint32_t STREAM_NOISE = 0x5A000000u;
+constexpr uint32_t STREAM_CHAN = 0xC4A00000u;
+constexpr uint32_t STREAM_START = 0x5B000000u;
+
+__device__ __forceinline__ uint4 philox10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                          uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)PHILOX_M0 * c0;   // v_mad_u64_u32
+        const uint64_t p1 = (uint64_t)PHILOX_M1 * c2;
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
+        k0 += PHILOX_W0; k1 += PHILOX_W1;
+    }
+    return make_uint4(c0, c1, c2, c3);
+}
+
+// Box-Muller pair.  u1 = fma((float)x1, 2^-32, 2^-33) in (0, 1] (tail to 6.7 sigma);
+// u2 = (float)x2 * 2^-32 in revolutions.  Same quantisation as oracle/ofdm_oracle.c:bm_pair.
+__device__ __forceinline__ float2 box_muller(uint32_t x1, uint32_t x2) {
+    const float u1 = fmaf((float)x1, 0x1p-32f, 0x1p-33f);
+    const float u2 = (float)x2 * 0x1p-32f;
+    // -2 ln(u1) = -2 ln(2) log2(u1)
+    const float r = __builtin_amdgcn_sqrtf(-1.38629436111989061883f * __builtin_amdgcn_logf(u1));
+    return make_float2(r * __builtin_amdgcn_cosf(u2), r * __builtin_amdgcn_sinf(u2));
+}
+
+// four N(0,1) draws of one Philox block
+struct Gauss4 { float z[4]; };
+__device__ __forceinline__ Gauss4 gauss4(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                         uint32_t k0, uint32_t k1) {
+    const uint4 o = philox10(c0, c1, c2, c3, k0, k1);
+    const float2 a = box_muller(o.x, o.y), b = box_muller(o.z, o.w);
+    Gauss4 g;
+    g.z[0] = a.x; g.z[1] = a.y; g.z[2] = b.x; g.z[3] = b.y;
+    return g;
+}
+
+// ------------------------------------------------------------------ twiddles
+// multiply by e^{-j 2 pi E / 64} (forward) or e^{+j 2 pi E / 64} (inverse); trivial cases free
+template <int E, bool INV>
+__device__ __forceinline__ float2 twiddle(float2 a) {
+    constexpr int e = ((E % 64) + 64) % 64;
+    if constexpr (e == 0) {
+        return a;
+    } else if constexpr (e == 32) {
+        return make_float2(-a.x, -a.y);
+    } else if constexpr ((e == 16 && !INV) || (e == 48 && INV)) {   // * (-j)
+        return make_float2(a.y, -a.x);
+    } else if constexpr ((e == 48 && !INV) || (e == 16 && INV)) {   // * (+j)
+        return make_float2(-a.y, a.x);
+    } else {
+        constexpr float wr = kCos64[e];
+        constexpr float wi = INV ? kSin64[e] : -kSin64[e];
+        return make_float2(fmaf(a.x, wr, -a.y * wi), fmaf(a.x, wi, a.y * wr));
+    }
+}
+
+// ------------------------------------------------------------------ radix-4 DIF 64-point FFT
+// x[k] natural order in; out: bin k at position digit_rev4(k).  Unnormalised.
+// Forward: X[k] = sum x[n] e^{-j2pi kn/64}; inverse: e^{+j...}.
+// The transform is exposed in pieces so callers can bound register live ranges:
+//   dif_bfly<INV, N, B, j>  one radix-4 butterfly (+ twiddles) of the stage of span N at offset B
+//   dif_stage1<INV, j>      butterfly j (0..15) of the first 64-point stage
+//   dif_sub16<INV, R>       the remaining two stages of sub-block R (positions 16R..16R+15);
+//                           afterwards bins k with (k & 3) == R are final.
+template <bool INV, int N, int B, int j>
+__device__ __forceinline__ void dif_bfly(float2 (&x)[64]) {
+    constexpr int Q = N / 4;
+    constexpr int S = 64 / N;
+    const float2 a = x[B + j], b = x[B + j + Q], c = x[B + j + 2 * Q], d = x[B + j + 3 * Q];
+    const float2 t0 = cadd(a, c), t1 = csub(a, c), t2 = cadd(b, d), t3 = csub(b, d);
+    float2 y1, y3;
+    if constexpr (!INV) {
+        y1 = make_float2(t1.x + t3.y, t1.y - t3.x);   // t1 - j t3
+        y3 = make_float2(t1.x - t3.y, t1.y + t3.x);   // t1 + j t3
+    } else {
+        y1 = make_float2(t1.x - t3.y, t1.y + t3.x);
+        y3 = make_float2(t1.x + t3.y, t1.y - t3.x);
+    }
+    x[B + j] = cadd(t0, t2);
+    x[B + j + Q] = twiddle<j * S, INV>(y1);
+    x[B + j + 2 * Q] = twiddle<2 * j * S, INV>(csub(t0, t2));
+    x[B + j + 3 * Q] = twiddle<3 * j * S, INV>(y3);
+}
+
+template <bool INV, int N, int B>
+__device__ __forceinline__ void dif4(float2 (&x)[64]) {
+    if constexpr (N >= 4) {
+        constexpr int Q = N / 4;
+        static_for<0, Q>([&](auto jc) { dif_bfly<INV, N, B, decltype(jc)::value>(x); });
+        dif4<INV, Q, B>(x);
+        dif4<INV, Q, B + Q>(x);
+        dif4<INV, Q, B + 2 * Q>(x);
+        dif4<INV, Q, B + 3 * Q>(x);
+    }
+}
+
+template <bool INV, int j>
+__device__ __forceinline__ void dif_stage1(float2 (&x)[64]) { dif_bfly<INV, 64, 0, j>(x); }
+template <bool INV, int R>
+__device__ __forceinline__ void dif_sub16(float2 (&x)[64]) { dif4<INV, 16, 16 * R>(x); }
+
+#ifndef OFDM_NO_SCHED_FENCE
+__device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
+#else
+__device__ __forceinline__ void sched_fence() {}
+#endif
+
+// Hide a value from the optimiser for one program point.  Used inside the per-SNR loop so that
+// loop-invariant work (64 load addresses, 96 truth-symbol selects, the first Philox round) is
+// recomputed each iteration instead of being hoisted and held in ~200 extra VGPRs.
+template <typename T>
+__device__ __forceinline__ void opaque(T &v) { asm volatile("" : "+v"(v)); }
+
+// global-address-space views (keep loads global_* after opaque(), which erases provenance).
+// Native clang vectors, not float2 (HIP_vector_type's members are not address-space qualified).
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) const f2v gcf2;
+typedef __attribute__((address_space(1))) f2v gf2;
+__device__ __forceinline__ float2 gld(gcf2 *p, int i) { const f2v v = p[i]; return make_float2(v.x, v.y); }
+__device__ __forceinline__ void gst(gf2 *p, int i, float2 v) { f2v t; t.x = v.x; t.y = v.y; p[i] = t; }
+
+// ------------------------------------------------------------------ wave64 reductions via DPP
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+constexpr int DPP_QUAD_XOR1 = 0xB1;      // quad_perm [1,0,3,2]
+constexpr int DPP_QUAD_XOR2 = 0x4E;      // quad_perm [2,3,0,1]
+constexpr int DPP_ROW_HALF_MIRROR = 0x141;
+constexpr int DPP_ROW_MIRROR = 0x140;
+
+// every lane ends with its 16-lane row sum; the four row sums are read with v_readlane
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+    v += dpp_u<DPP_QUAD_XOR1>(v);
+    v += dpp_u<DPP_QUAD_XOR2>(v);
+    v += dpp_u<DPP_ROW_HALF_MIRROR>(v);
+    v += dpp_u<DPP_ROW_MIRROR>(v);
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) + (uint32_t)__builtin_amdgcn_readlane((int)v, 16) +
+           (uint32_t)__builtin_amdgcn_readlane((int)v, 32) + (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+}
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t v) {
+    return ((uint64_t)dpp_u<CTRL>((uint32_t)(v >> 32)) << 32) | dpp_u<CTRL>((uint32_t)v);
+}
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+    v += dpp_u64<DPP_QUAD_XOR1>(v);
+    v += dpp_u64<DPP_QUAD_XOR2>(v);
+    v += dpp_u64<DPP_ROW_HALF_MIRROR>(v);
+    v += dpp_u64<DPP_ROW_MIRROR>(v);
+    uint64_t t = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 16 * r);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 16 * r);
+        t += ((uint64_t)hi << 32) | lo;
+    }
+    return t;
+}
+
+__host__ __device__ constexpr int digit_rev4(int k) {
+    return ((k & 3) << 4) | (k & 12) | ((k >> 4) & 3);
+}
+
+template <bool INV>
+__device__ __forceinline__ void fft64(float2 (&x)[64]) { dif4<INV, 64, 0>(x); }
+
+// ------------------------------------------------------------------ 802.11a subcarrier plan
+// fftshifted bin of data subcarrier m (OFDM.c:528-547 Tx, 1063-1068 Rx)
+__host__ __device__ constexpr int data_bin(int m) {
+    return m < 5 ? 6 + m : m < 18 ? 7 + m : m < 24 ? 8 + m : m < 30 ? 9 + m : m < 43 ? 10 + m : 11 + m;
+}
+// inverse: data subcarrier index of an fftshifted bin, -1 for pilots / nulls / DC
+__host__ __device__ constexpr int data_index(int bin) {
+    return (bin >= 6 && bin <= 10) ? bin - 6 : (bin >= 12 && bin <= 24) ? bin - 7 : (bin >= 26 && bin <= 31) ? bin - 8
+         : (bin >= 33 && bin <= 38) ? bin - 9 : (bin >= 40 && bin <= 52) ? bin - 10 : (bin >= 54 && bin <= 58) ? bin - 11 : -1;
+}
+// pilots {1,1,1,-1} at bins 11,25,39,53 (OFDM.c:523,531-544)
+__host__ __device__ constexpr float pilot_at(int bin) {
+    return bin == 11 || bin == 25 || bin == 39 ? 1.0f : (bin == 53 ? -1.0f : 0.0f);
+}
+// long training tones L_k at bins 6..58 (OFDM.c:494) -- sign on the data bins (all +-1)
+__host__ __device__ constexpr int ltf_sign(int bin) {
+    constexpr int8_t L[53] = {1, 1, -1, -1, 1, 1, -1, 1, -1, 1, 1, 1, 1, 1, 1, -1, -1, 1, 1, -1, 1, -1, 1, 1,
+                              1, 1, 0, 1, -1, -1, 1, 1, -1, 1, -1, 1, -1, -1, -1, -1, -1, 1, 1, -1, -1, 1,
+                              -1, 1, -1, 1, 1, 1, 1};
+    return (bin >= 6 && bin <= 58) ? L[bin - 6] : 0;
+}
+
+constexpr float INV_SQRT2 = 0.70710678118654752440f;
+
+// bit b (0..95) of a symbol's 3 MSB-first words
+__device__ __forceinline__ uint32_t bit_of(const uint32_t w[3], int b) {
+    return (w[b >> 5] >> (31 - (b & 31))) & 1u;
+}
+
+}  // namespace ofdm

@@ -1,0 +1,580 @@
+// ofdm_symbol.hip -- symbol-mode kernels for gfx950 (MI355X): K1 batched FFT, K2 Tx builder,
+// K3 fused AWGN/Rayleigh + receiver chain with counters.  DESIGN.md §2-§4 describe layout,
+// roofline and the RNG spec; the per-stage reference lines are cited inline.
+//
+// Mapping: ONE LANE OWNS ONE 64-SAMPLE WINDOW (a data symbol or one long-training symbol); its
+// 64-point FFT lives in that lane's VGPRs (ofdm_device.h).  In LS mode the four lanes of a DPP
+// quad carry one frame {LTF1, LTF2, D0, D1}: the LS estimate H = 0.5(F1+F2)conj(Lf)
+// (OFDM.c:830-850) is formed with two quad broadcasts, no LDS.
+//
+// Register discipline: the first radix-4 stage is fused with sample generation (load + channel +
+// noise) four butterflies at a time, then the four 16-point sub-FFTs run one after another and
+// each sub-block's bins are consumed (demapped or stored) at once.  sched_fence() pins that
+// order so the live set stays ~128 VGPRs + temporaries (3 waves/SIMD, no scratch).
+#include "ofdm_internal.h"
+
+#ifndef OFDM_RX_WAVES_PER_SIMD
+#define OFDM_RX_WAVES_PER_SIMD 2
+#endif
+
+namespace ofdm {
+
+// ======================================================================== K1: batched FFT
+// One wave = 64 transforms.  Coalesced 16-B loads into a padded LDS image (row = 64 float2 + 1
+// pad: conflict-free ds_read_b64 per lane-row), each lane then runs its own register FFT.
+constexpr int K1_ROW = 65;  // float2 per LDS row
+
+template <bool INV, int CONV>
+__global__ __launch_bounds__(64, 2) void fft64_kernel(const float2 *__restrict__ in, float2 *__restrict__ out,
+                                                      int64_t n) {
+    __shared__ float2 lds[64 * K1_ROW];
+    const int lane = threadIdx.x;
+    const int64_t base = (int64_t)blockIdx.x * 64;
+    const int64_t nt = (n - base) < 64 ? (n - base) : 64;   // transforms in this wave
+    const float4 *src = reinterpret_cast<const float4 *>(in + base * 64);
+#pragma unroll 8
+    for (int k = 0; k < 32; ++k) {
+        const int e = k * 128 + lane * 2;   // float2 element index within the wave's block
+        const int row = e >> 6, col = e & 63;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (row < nt) v = src[e >> 1];
+        lds[row * K1_ROW + col] = make_float2(v.x, v.y);
+        lds[row * K1_ROW + col + 1] = make_float2(v.z, v.w);
+    }
+    __syncthreads();
+    float2 x[64];
+    const float2 *row = lds + lane * K1_ROW;
+    static_for<0, 4>([&](auto gc) {
+        constexpr int g = decltype(gc)::value;
+        static_for<0, 16>([&](auto pc) {
+            constexpr int n = 16 * (decltype(pc)::value >> 2) + 4 * g + (decltype(pc)::value & 3);
+            float2 v = row[n];
+            // fft(): DFT of x[n](-1)^n = fftshift(DFT(x)) (OFDM.c:314-318);
+            // ifft(): X~[i] = X[i](-1)^i for the C convention (D5), none for MATLAB
+            if constexpr ((!INV || CONV == OFDM_CONV_C) && (n & 1)) v = make_float2(-v.x, -v.y);
+            x[n] = v;
+        });
+        static_for<0, 4>([&](auto ic) { dif_stage1<INV, 4 * g + decltype(ic)::value>(x); });
+        sched_fence();
+    });
+    __syncthreads();   // every lane has read its row
+    float2 *orow = lds + lane * K1_ROW;
+    static_for<0, 4>([&](auto rc) {
+        constexpr int R = decltype(rc)::value;
+        dif_sub16<INV, R>(x);
+        static_for<0, 16>([&](auto kc) {
+            constexpr int k = 4 * decltype(kc)::value + R;     // bins with k & 3 == R
+            float2 v = x[digit_rev4(k)];
+            if constexpr (INV) v = cscale(v, (k & 1) ? -1.0f / 64.0f : 1.0f / 64.0f);   // (-1)^n / 64
+            orow[k] = v;
+        });
+        sched_fence();
+    });
+    __syncthreads();
+    float4 *dst = reinterpret_cast<float4 *>(out + base * 64);
+#pragma unroll 8
+    for (int k = 0; k < 32; ++k) {
+        const int e = k * 128 + lane * 2;
+        const int r = e >> 6, col = e & 63;
+        if (r < nt) {
+            const float2 a = lds[r * K1_ROW + col], b = lds[r * K1_ROW + col + 1];
+            dst[e >> 1] = make_float4(a.x, a.y, b.x, b.y);
+        }
+    }
+}
+
+// ======================================================================== K2: Tx builder
+// One lane = one data symbol: bits -> QPSK (OFDM.c:415-433) -> subcarrier map + pilots
+// (OFDM.c:523-548) -> ifft (OFDM.c:320-339, convention D5) -> CP (OFDM.c:559-565) -> HBM.
+template <int CONV, int BIN>
+__device__ __forceinline__ float2 tx_bin(const uint32_t (&w)[3]) {
+    constexpr float sgn = (CONV == OFDM_CONV_C && (BIN & 1)) ? -1.0f : 1.0f;   // ifftshift+fftshift (D5)
+    constexpr int m = data_index(BIN);
+    if constexpr (m >= 0) {
+        const uint32_t b0 = bit_of(w, 2 * m), b1 = bit_of(w, 2 * m + 1);
+        // 00:(+,+) 01:(-,+) 10:(-,-) 11:(+,-): re > 0 iff b0 == b1, im > 0 iff b0 == 0 (D10)
+        const float re = (b0 == b1) ? sgn * INV_SQRT2 : -sgn * INV_SQRT2;
+        const float im = b0 ? -sgn * INV_SQRT2 : sgn * INV_SQRT2;
+        return make_float2(re, im);
+    } else {
+        return make_float2(sgn * pilot_at(BIN), 0.0f);    // pilots {1,1,1,-1}; nulls and DC 0
+    }
+}
+
+template <int CONV>
+__global__ __launch_bounds__(256, 3) void tx_symbols_kernel(TxArgs a) {
+    const int64_t sidx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // symbol within batch
+    if (sidx >= a.n_sym) return;
+    const uint64_t s = a.first_symbol + (uint64_t)sidx;
+    uint32_t w[3];
+    if (a.payload == OFDM_PAYLOAD_RANDOM) {
+        const uint4 o = philox10((uint32_t)s, (uint32_t)(s >> 32), 0u, STREAM_BITS, a.k0, a.k1);
+        w[0] = o.x; w[1] = o.y; w[2] = o.z;
+    } else {
+        const int r = (int)(s & 1);
+        w[0] = a.table[3 * r]; w[1] = a.table[3 * r + 1]; w[2] = a.table[3 * r + 2];
+    }
+    float2 X[64];
+    static_for<0, 4>([&](auto gc) {
+        constexpr int g = decltype(gc)::value;
+        uint32_t wg[3] = {w[0], w[1], w[2]};
+        opaque(wg[0]); opaque(wg[1]); opaque(wg[2]);
+        static_for<0, 16>([&](auto pc) {
+            constexpr int i = 16 * (decltype(pc)::value >> 2) + 4 * g + (decltype(pc)::value & 3);
+            X[i] = tx_bin<CONV, i>(wg);
+        });
+        static_for<0, 4>([&](auto ic) { dif_stage1<true, 4 * g + decltype(ic)::value>(X); });
+        sched_fence();
+    });
+    const int64_t tile = sidx >> 5;
+    const int slot = (int)(sidx & 31);
+    float2 *dst = a.tx + tile * (SYM_SAMPLES * TILE_SYMBOLS) + slot;
+    static_for<0, 4>([&](auto rc) {
+        constexpr int R = decltype(rc)::value;
+        dif_sub16<true, R>(X);
+        gf2 *d = (gf2 *)dst;
+        opaque(d);
+        static_for<0, 16>([&](auto nc) {
+            constexpr int n = 4 * decltype(nc)::value + R;                   // time samples n & 3 == R
+            const float2 v = cscale(X[digit_rev4(n)], (n & 1) ? -1.0f / 64.0f : 1.0f / 64.0f);
+            gst(d, (16 + n) * TILE_SYMBOLS, v);
+            if constexpr (n >= 48) gst(d, (n - 48) * TILE_SYMBOLS, v);           // CP = last 16 samples
+        });
+        sched_fence();
+    });
+    uint32_t *bd = a.bits + tile * (3 * TILE_SYMBOLS) + slot;
+    bd[0] = w[0]; bd[TILE_SYMBOLS] = w[1]; bd[2 * TILE_SYMBOLS] = w[2];
+}
+
+// ======================================================================== K3: receiver chain
+// Clean sample n of a window: data windows read row 16+n of the Tx tile (n >= -3 reaches into the
+// CP), LTF windows read the cyclic training symbol T[(n + 64) & 63].
+struct WindowSrc {
+    gcf2 *p;             // data: &tile[16][slot]; LTF: T
+    int stride;          // 32 (data) or 1 (LTF)
+    bool circ;           // LTF
+};
+__device__ __forceinline__ float2 src_at(gcf2 *p, int stride, bool circ, int n) {
+    if (n >= 0) return gld(p, n * stride);
+    return circ ? gld(p, 64 + n) : gld(p, n * stride);
+}
+
+// Load + channel + AWGN for samples n0..n0+3, times (-1)^n (fft() = DFT of x(-1)^n, OFDM.c:314-318).
+// Noise sample at frame time t uses Gaussian t (real) or 2t, 2t+1 (complex) of the frame's stream
+// (DESIGN.md §3); AWGN is real-only as OFDM.c:651 really does (D7).
+template <int NOISE, int CHAN, int N0>
+__device__ __forceinline__ void rx_block(float2 (&x)[64], const WindowSrc &src, uint32_t f_lo, uint32_t f_hi,
+                                         uint32_t t0, uint32_t q, float sigma, uint32_t k0, uint32_t k1,
+                                         const float2 (&h)[4]) {
+    // re-materialise per block: keeps LICM from hoisting 16 blocks' worth of addresses / round-1 products
+    gcf2 *p = src.p;
+    uint32_t flo = f_lo, fhi = f_hi, tb = t0;
+    opaque(p); opaque(flo); opaque(fhi); opaque(tb);
+    f_lo = flo; f_hi = fhi; t0 = tb;
+    float z[8];
+    if constexpr (NOISE == OFDM_NOISE_REAL) {
+        const Gauss4 g = gauss4(f_lo, f_hi, (t0 >> 2) + (N0 >> 2), STREAM_NOISE | q, k0, k1);
+        z[0] = g.z[0]; z[1] = g.z[1]; z[2] = g.z[2]; z[3] = g.z[3];
+    } else if constexpr (NOISE == OFDM_NOISE_COMPLEX) {
+        const Gauss4 g0 = gauss4(f_lo, f_hi, (t0 >> 1) + (N0 >> 1), STREAM_NOISE | q, k0, k1);
+        const Gauss4 g1 = gauss4(f_lo, f_hi, (t0 >> 1) + (N0 >> 1) + 1, STREAM_NOISE | q, k0, k1);
+        z[0] = g0.z[0]; z[1] = g0.z[1]; z[2] = g0.z[2]; z[3] = g0.z[3];
+        z[4] = g1.z[0]; z[5] = g1.z[1]; z[6] = g1.z[2]; z[7] = g1.z[3];
+    }
+    float2 c[7];
+    if constexpr (CHAN == OFDM_CHAN_RAYLEIGH4) {
+        static_for<0, 7>([&](auto ic) { c[decltype(ic)::value] = src_at(p, src.stride, src.circ, N0 - 3 + decltype(ic)::value); });
+    } else {
+        static_for<0, 4>([&](auto ic) { c[3 + decltype(ic)::value] = src_at(p, src.stride, src.circ, N0 + decltype(ic)::value); });
+    }
+    static_for<0, 4>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        constexpr int n = N0 + i;
+        float2 y = c[3 + i];
+        if constexpr (CHAN == OFDM_CHAN_RAYLEIGH4) {   // y[t] = sum_l h_l x[t - l], 4 taps < CP
+            y = cadd(cadd(cmul(h[0], c[3 + i]), cmul(h[1], c[2 + i])), cadd(cmul(h[2], c[1 + i]), cmul(h[3], c[i])));
+        }
+        if constexpr (NOISE == OFDM_NOISE_REAL) {
+            y.x = fmaf(sigma, z[i], y.x);
+        } else if constexpr (NOISE == OFDM_NOISE_COMPLEX) {
+            const float sh = sigma * INV_SQRT2;
+            y.x = fmaf(sh, z[2 * i], y.x);
+            y.y = fmaf(sh, z[2 * i + 1], y.y);
+        }
+        if constexpr (n & 1) y = make_float2(-y.x, -y.y);
+        x[n] = y;
+    });
+}
+
+// generate the window fused with the first radix-4 stage (4 butterflies per group)
+template <int NOISE, int CHAN>
+__device__ __forceinline__ void rx_window_stage1(float2 (&x)[64], const WindowSrc &src, uint32_t f_lo,
+                                                 uint32_t f_hi, uint32_t t0, uint32_t q, float sigma,
+                                                 uint32_t k0, uint32_t k1, const float2 (&h)[4]) {
+    static_for<0, 4>([&](auto gc) {
+        constexpr int g = decltype(gc)::value;
+        rx_block<NOISE, CHAN, 4 * g>(x, src, f_lo, f_hi, t0, q, sigma, k0, k1, h);
+        rx_block<NOISE, CHAN, 16 + 4 * g>(x, src, f_lo, f_hi, t0, q, sigma, k0, k1, h);
+        rx_block<NOISE, CHAN, 32 + 4 * g>(x, src, f_lo, f_hi, t0, q, sigma, k0, k1, h);
+        rx_block<NOISE, CHAN, 48 + 4 * g>(x, src, f_lo, f_hi, t0, q, sigma, k0, k1, h);
+        static_for<0, 4>([&](auto ic) { dif_stage1<false, 4 * g + decltype(ic)::value>(x); });
+        sched_fence();
+    });
+}
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ float2 dpp_c(float2 v) { return make_float2(dpp_f<CTRL>(v.x), dpp_f<CTRL>(v.y)); }
+constexpr int DPP_QUAD_BCAST0 = 0x00;   // quad_perm [0,0,0,0]
+constexpr int DPP_QUAD_BCAST1 = 0x55;   // quad_perm [1,1,1,1]
+
+__device__ __forceinline__ void channel_taps(uint32_t f_lo, uint32_t f_hi, uint32_t k0, uint32_t k1, float2 (&h)[4]) {
+    const Gauss4 a = gauss4(f_lo, f_hi, 0u, STREAM_CHAN, k0, k1);
+    const Gauss4 b = gauss4(f_lo, f_hi, 1u, STREAM_CHAN, k0, k1);
+    const float s = 0.35355339059327376220f;   // sqrt(1/8): CN(0, 1/4) per tap
+    h[0] = make_float2(s * a.z[0], s * a.z[1]);
+    h[1] = make_float2(s * a.z[2], s * a.z[3]);
+    h[2] = make_float2(s * b.z[0], s * b.z[1]);
+    h[3] = make_float2(s * b.z[2], s * b.z[3]);
+}
+
+// Per-symbol decisions + metrics, consumed one FFT sub-block at a time.
+//   Z = Y / H (OFDM.c:1044-1052), slicer (OFDM.c:852-871), demap (OFDM.c:873-908), bit compare
+//   (OFDM.c:1154-1161), EVM pre/post (OFDM.c:1104-1150).
+struct SymState { float evm_pre; uint32_t d[3]; };
+
+template <bool DUMP, int R, typename HF>
+__device__ __forceinline__ void demap_sub(const float2 (&x)[64], const uint32_t (&wi)[3], HF &&Hof, float2 *dump_eq,
+                                          SymState &st) {
+    uint32_t w[3] = {wi[0], wi[1], wi[2]};
+    opaque(w[0]); opaque(w[1]); opaque(w[2]);     // truth selects are made here, not hoisted
+    static_for<0, 16>([&](auto kc) {
+        constexpr int bin = 4 * decltype(kc)::value + R;
+        constexpr int m = data_index(bin);
+        if constexpr (m >= 0) {
+            const float2 z = Hof(x[digit_rev4(bin)], std::integral_constant<int, bin>{});
+            if constexpr (DUMP) { if (dump_eq) dump_eq[m] = z; }
+            const uint32_t pr = z.x > 0.f, pi = z.y > 0.f;
+            constexpr int s0 = 31 - ((2 * m) & 31), s1 = 31 - ((2 * m + 1) & 31), wi = (2 * m) >> 5;
+            st.d[wi] |= ((pi ^ 1u) << s0) | ((pr ^ pi) << s1);
+            const uint32_t b0 = bit_of(w, 2 * m), b1 = bit_of(w, 2 * m + 1);
+            const float dr = (b0 == b1) ? INV_SQRT2 : -INV_SQRT2;
+            const float di = b0 ? -INV_SQRT2 : INV_SQRT2;
+            const float ex = z.x - dr, ey = z.y - di;
+            st.evm_pre = fmaf(ex, ex, fmaf(ey, ey, st.evm_pre));
+        }
+    });
+}
+
+__device__ __forceinline__ void symbol_errors(const SymState &st, const uint32_t (&w)[3], uint32_t &be, uint32_t &ax) {
+    be = 0; ax = 0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const uint32_t e = st.d[i] ^ w[i];
+        const uint32_t e0 = e & 0xAAAAAAAAu, e1 = e & 0x55555555u;   // b0 (imag axis) / b1 positions
+        be += __popc(e);
+        ax += __popc(e0) + __popc((e0 >> 1) ^ e1);                     // im wrong + (re xor im) wrong
+    }
+}
+
+// frame-level counters of one wave, reduced and added into the block's LDS slots
+struct FrameAcc {
+    uint32_t bit_err = 0, frame_err = 0, axis = 0, post_finite = 0;
+    int64_t pre_q = 0, dbpre_q = 0, dbpost_q = 0;
+};
+
+__device__ __forceinline__ void frame_metrics(FrameAcc &acc, float fe_pre, uint32_t ferr, uint32_t fax) {
+    const float N = 96.0f;   // 48 subcarriers x D = 2
+    acc.bit_err += ferr;
+    acc.frame_err += ferr > 0u;
+    acc.axis += fax;
+    acc.pre_q += (int64_t)__float2ll_rn(fe_pre * (float)OFDM_EVM_Q_SCALE);
+    // per-frame EVM_dB = 10 log10(sum|e|^2 / sum|d|^2), |d| = 1 (OFDM.c:1124-1126), floor -400 dB
+    const float lg = 3.01029995663981195214f * __builtin_amdgcn_logf(fe_pre / N);   // 10 log10(2) log2
+    const float db = fe_pre > 0.f ? fmaxf(lg, -400.0f) : -400.0f;
+    acc.dbpre_q += (int64_t)__float2ll_rn(db * (float)OFDM_EVM_Q_SCALE);
+    if (fax > 0u) {
+        const float dbp = 3.01029995663981195214f * __builtin_amdgcn_logf(2.0f * (float)fax / N);
+        acc.dbpost_q += (int64_t)__float2ll_rn(dbp * (float)OFDM_EVM_Q_SCALE);
+        acc.post_finite += 1u;
+    }
+}
+
+
+__device__ __forceinline__ void flush_wave(const FrameAcc &acc, unsigned long long *slots /*[8]*/) {
+    // per wave and SNR: bit_err, axis <= 32 frames x 192 < 2^16; frame counts <= 32
+    const uint32_t p0 = wave_sum_u32(acc.bit_err | (acc.axis << 16));
+    const uint32_t p1 = wave_sum_u32(acc.frame_err | (acc.post_finite << 16));
+    const uint32_t a0 = p0 & 0xFFFFu, a2 = p0 >> 16, a1 = p1 & 0xFFFFu, a3 = p1 >> 16;
+    const uint64_t b0 = wave_sum_u64((uint64_t)acc.pre_q), b1 = wave_sum_u64((uint64_t)acc.dbpre_q);
+    const uint64_t b2 = wave_sum_u64((uint64_t)acc.dbpost_q);
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&slots[0], (unsigned long long)a0);
+        atomicAdd(&slots[1], (unsigned long long)a1);
+        atomicAdd(&slots[2], (unsigned long long)a2);
+        atomicAdd(&slots[3], (unsigned long long)a3);
+        atomicAdd(&slots[4], (unsigned long long)b0);
+        atomicAdd(&slots[5], (unsigned long long)b1);
+        atomicAdd(&slots[6], (unsigned long long)b2);
+    }
+}
+
+// LDS slot k -> counter index
+__device__ __forceinline__ int slot_counter(int k) {
+    return k == 0 ? OFDM_C_BIT_ERR : k == 1 ? OFDM_C_FRAME_ERR : k == 2 ? OFDM_C_EVM_POST_AXIS
+         : k == 3 ? OFDM_C_EVMDB_POST_FINITE : k == 4 ? OFDM_C_EVM_PRE_Q : k == 5 ? OFDM_C_EVMDB_PRE_Q
+         : OFDM_C_EVMDB_POST_Q;
+}
+
+__device__ __forceinline__ void block_flush(const RxArgs &a, unsigned long long (*sacc)[8]) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < a.n_snr * 7; i += blockDim.x) {
+        const int q = i / 7, k = i % 7;
+        const unsigned long long v = sacc[q][k];
+        if (v) atomicAdd(&a.counters[q * OFDM_NCOUNTERS + slot_counter(k)], v);
+    }
+    if (blockIdx.x == 0) {
+        for (int q = threadIdx.x; q < a.n_snr; q += blockDim.x) {
+            unsigned long long *c = a.counters + q * OFDM_NCOUNTERS;
+            atomicAdd(&c[OFDM_C_FRAMES], (unsigned long long)a.n_frames);
+            atomicAdd(&c[OFDM_C_SYMBOLS], (unsigned long long)(2 * a.n_frames));
+            atomicAdd(&c[OFDM_C_BITS], (unsigned long long)(192 * a.n_frames));
+            atomicAdd(&c[OFDM_C_EVM_TERMS], (unsigned long long)(96 * a.n_frames));
+        }
+    }
+}
+
+// Shared tail: FFT sub-blocks + demap, per-frame combine of the two data symbols (quad xor-1
+// partner), counters.  `leader` lanes (one per valid frame) contribute.
+template <bool DUMP, typename HF>
+__device__ __forceinline__ void finish_symbol(float2 (&x)[64], const uint32_t (&w)[3], HF &&Hof, float2 *dump_eq,
+                                              uint32_t *dump_bits, bool leader, unsigned long long *slots) {
+    SymState st;
+    st.evm_pre = 0.f;
+    st.d[0] = st.d[1] = st.d[2] = 0u;
+    static_for<0, 4>([&](auto rc) {
+        constexpr int R = decltype(rc)::value;
+        dif_sub16<false, R>(x);
+        demap_sub<DUMP, R>(x, w, Hof, dump_eq, st);
+        sched_fence();
+    });
+    if constexpr (DUMP) {
+        if (dump_bits) { dump_bits[0] = st.d[0]; dump_bits[1] = st.d[1]; dump_bits[2] = st.d[2]; }
+    }
+    uint32_t be, ax;
+    symbol_errors(st, w, be, ax);
+    const float e_other = dpp_f<DPP_QUAD_XOR1>(st.evm_pre);
+    const uint32_t be_other = dpp_u<DPP_QUAD_XOR1>(be);
+    const uint32_t ax_other = dpp_u<DPP_QUAD_XOR1>(ax);
+    FrameAcc acc;
+    if (leader) frame_metrics(acc, st.evm_pre + e_other, be + be_other, ax + ax_other);
+    flush_wave(acc, slots);
+}
+
+// ---- LS estimate: quad = {LTF1, LTF2, D0, D1} of one frame; wave = 16 frames = one tile ----
+template <int NOISE, int CHAN, bool DUMP>
+__global__ __launch_bounds__(256, OFDM_RX_WAVES_PER_SIMD) void rx_ls_kernel(RxArgs a) {
+    __shared__ unsigned long long sacc[OFDM_MAX_SNR][8];
+    for (int i = threadIdx.x; i < a.n_snr * 8; i += blockDim.x) (&sacc[0][0])[i] = 0ull;
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int role = lane & 3, fi = lane >> 2;
+    const int64_t wave_id = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t n_waves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    // window start on the frame timeline: LTF1 192, LTF2 256, D0 336, D1 416
+    const uint32_t t0 = role == 0 ? 192u : role == 1 ? 256u : (role == 2 ? 336u : 416u);
+    const bool is_data = role >= 2;
+    const int slot = 2 * fi + (role & 1);
+
+    for (int64_t tile = wave_id; tile < a.n_tiles; tile += n_waves) {
+        const int64_t fl = tile * TILE_FRAMES + fi;
+        const bool valid = fl < a.n_frames;
+        const uint64_t f = a.first_frame + (uint64_t)fl;
+        const uint32_t f_lo = (uint32_t)f, f_hi = (uint32_t)(f >> 32);
+        WindowSrc src;
+        src.p = (gcf2 *)(is_data ? a.tx + tile * (SYM_SAMPLES * TILE_SYMBOLS) + 16 * TILE_SYMBOLS + slot : a.ltf);
+        src.stride = is_data ? TILE_SYMBOLS : 1;
+        src.circ = !is_data;
+        uint32_t w[3] = {0u, 0u, 0u};
+        if (is_data) {
+            const uint32_t *bp = a.bits + tile * (3 * TILE_SYMBOLS) + slot;
+            w[0] = bp[0]; w[1] = bp[TILE_SYMBOLS]; w[2] = bp[2 * TILE_SYMBOLS];
+        }
+        float2 h[4] = {make_float2(1.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f)};
+        if constexpr (CHAN == OFDM_CHAN_RAYLEIGH4) channel_taps(f_lo, f_hi, a.k0, a.k1, h);
+
+        for (int q = 0; q < a.n_snr; ++q) {
+            WindowSrc s = src;
+            uint32_t wq[3] = {w[0], w[1], w[2]};
+            uint32_t flo = f_lo, fhi = f_hi;
+            float2 hq[4] = {h[0], h[1], h[2], h[3]};
+            opaque(s.p); opaque(wq[0]); opaque(wq[1]); opaque(wq[2]); opaque(flo); opaque(fhi);
+            if constexpr (CHAN == OFDM_CHAN_RAYLEIGH4) {
+                static_for<0, 4>([&](auto lc) { opaque(hq[decltype(lc)::value].x); opaque(hq[decltype(lc)::value].y); });
+            }
+            float2 x[64];
+            rx_window_stage1<NOISE, CHAN>(x, s, flo, fhi, t0, (uint32_t)(a.q_base + q), a.sigma[q], a.k0, a.k1, hq);
+            float2 *dump_eq = nullptr;
+            uint32_t *dump_bits = nullptr;
+            if constexpr (DUMP) {
+                if (is_data && valid) {
+                    const int64_t r = ((int64_t)q * a.dump_frames + fl) * 2 + (role & 1);
+                    dump_eq = a.dump_eq + r * 48;
+                    dump_bits = a.dump_bits + r * 3;
+                }
+            }
+            // H[k] = 0.5 (F1[k] + F2[k]) conj(Lf[k]), Lf = +-1 on data bins (OFDM.c:846-849)
+            auto Hof = [&](float2 Y, auto binc) {
+                constexpr int bin = decltype(binc)::value;
+                constexpr float hs = 0.5f * (float)ltf_sign(bin);
+                const float2 F1 = dpp_c<DPP_QUAD_BCAST0>(Y), F2 = dpp_c<DPP_QUAD_BCAST1>(Y);
+                const float2 H = make_float2(hs * (F1.x + F2.x), hs * (F1.y + F2.y));
+                const float inv = __builtin_amdgcn_rcpf(fmaf(H.x, H.x, H.y * H.y));
+                return cscale(cmulc(Y, H), inv);
+            };
+            finish_symbol<DUMP>(x, wq, Hof, dump_eq, dump_bits, role == 2 && valid, sacc[q]);
+        }
+    }
+    block_flush(a, sacc);
+}
+
+// ---- ideal channel knowledge: every lane a data symbol; wave = 2 tiles = 32 frames ----
+template <int CONV, int NOISE, int CHAN, bool DUMP>
+__global__ __launch_bounds__(256, OFDM_RX_WAVES_PER_SIMD) void rx_ideal_kernel(RxArgs a) {
+    __shared__ unsigned long long sacc[OFDM_MAX_SNR][8];
+    for (int i = threadIdx.x; i < a.n_snr * 8; i += blockDim.x) (&sacc[0][0])[i] = 0ull;
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int64_t wave_id = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t n_waves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    const int d = lane & 1;
+    const uint32_t t0 = 336u + 80u * (uint32_t)d;
+    const int64_t n_pairs = (a.n_tiles + 1) >> 1;
+    for (int64_t pr = wave_id; pr < n_pairs; pr += n_waves) {
+        const int64_t tile = 2 * pr + (lane >> 5);
+        const int slot = lane & 31;
+        const int64_t fl = tile * TILE_FRAMES + (slot >> 1);
+        const bool valid = fl < a.n_frames;
+        const uint64_t f = a.first_frame + (uint64_t)fl;
+        const uint32_t f_lo = (uint32_t)f, f_hi = (uint32_t)(f >> 32);
+        WindowSrc src;
+        src.p = (gcf2 *)(a.tx + tile * (SYM_SAMPLES * TILE_SYMBOLS) + 16 * TILE_SYMBOLS + slot);
+        src.stride = TILE_SYMBOLS;
+        src.circ = false;
+        const uint32_t *bp = a.bits + tile * (3 * TILE_SYMBOLS) + slot;
+        uint32_t w[3] = {bp[0], bp[TILE_SYMBOLS], bp[2 * TILE_SYMBOLS]};
+        float2 h[4] = {make_float2(1.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f)};
+        if constexpr (CHAN == OFDM_CHAN_RAYLEIGH4) channel_taps(f_lo, f_hi, a.k0, a.k1, h);
+        for (int q = 0; q < a.n_snr; ++q) {
+            WindowSrc s = src;
+            uint32_t wq[3] = {w[0], w[1], w[2]};
+            uint32_t flo = f_lo, fhi = f_hi;
+            float2 hq[4] = {h[0], h[1], h[2], h[3]};
+            opaque(s.p); opaque(wq[0]); opaque(wq[1]); opaque(wq[2]); opaque(flo); opaque(fhi);
+            if constexpr (CHAN == OFDM_CHAN_RAYLEIGH4) {
+                static_for<0, 4>([&](auto lc) { opaque(hq[decltype(lc)::value].x); opaque(hq[decltype(lc)::value].y); });
+            }
+            float2 x[64];
+            rx_window_stage1<NOISE, CHAN>(x, s, flo, fhi, t0, (uint32_t)(a.q_base + q), a.sigma[q], a.k0, a.k1, hq);
+            float2 *dump_eq = nullptr;
+            uint32_t *dump_bits = nullptr;
+            if constexpr (DUMP) {
+                if (valid) {
+                    const int64_t r = ((int64_t)q * a.dump_frames + fl) * 2 + d;
+                    dump_eq = a.dump_eq + r * 48;
+                    dump_bits = a.dump_bits + r * 3;
+                }
+            }
+            // perfect CSI: H[i] = c_i sum_l h_l e^{-j2pi(i-32)l/64}, c_i = (-1)^i for the C ifft (D5)
+            auto Hof = [&](float2 Y, auto binc) {
+                constexpr int bin = decltype(binc)::value;
+                constexpr float cs = (CONV == OFDM_CONV_C && (bin & 1)) ? -1.0f : 1.0f;
+                if constexpr (CHAN == OFDM_CHAN_AWGN) {
+                    return cscale(Y, cs);
+                } else {
+                    float2 H = hq[0];
+                    H = csub(H, twiddle<bin * 1, false>(hq[1]));     // e^{-j2pi(i-32)l/64} = (-1)^l W^{il}
+                    H = cadd(H, twiddle<bin * 2, false>(hq[2]));
+                    H = csub(H, twiddle<bin * 3, false>(hq[3]));
+                    H = cscale(H, cs);
+                    const float inv = __builtin_amdgcn_rcpf(fmaf(H.x, H.x, H.y * H.y));
+                    return cscale(cmulc(Y, H), inv);
+                }
+            };
+            finish_symbol<DUMP>(x, wq, Hof, dump_eq, dump_bits, d == 0 && valid, sacc[q]);
+        }
+    }
+    block_flush(a, sacc);
+}
+
+// ======================================================================== launchers
+template <bool INV>
+static void launch_fft_conv(int conv, dim3 g, hipStream_t st, const float2 *in, float2 *out, int64_t n) {
+    if (conv == OFDM_CONV_C) hipLaunchKernelGGL((fft64_kernel<INV, OFDM_CONV_C>), g, dim3(64), 0, st, in, out, n);
+    else hipLaunchKernelGGL((fft64_kernel<INV, OFDM_CONV_MATLAB>), g, dim3(64), 0, st, in, out, n);
+}
+
+void launch_fft64(hipStream_t st, const float2 *in, float2 *out, int64_t n, int inverse, int conv) {
+    const dim3 g((unsigned)((n + 63) / 64));
+    if (inverse) launch_fft_conv<true>(conv, g, st, in, out, n);
+    else launch_fft_conv<false>(OFDM_CONV_C, g, st, in, out, n);
+}
+
+void launch_tx(hipStream_t st, const TxArgs &a, int conv) {
+    const dim3 g((unsigned)((a.n_sym + 255) / 256));
+    if (conv == OFDM_CONV_C) hipLaunchKernelGGL(tx_symbols_kernel<OFDM_CONV_C>, g, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(tx_symbols_kernel<OFDM_CONV_MATLAB>, g, dim3(256), 0, st, a);
+}
+
+template <int NOISE, int CHAN, bool DUMP>
+static void launch_rx_t(hipStream_t st, const RxArgs &a, int est, int conv, unsigned grid) {
+    if (est == OFDM_EST_LS) {
+        hipLaunchKernelGGL((rx_ls_kernel<NOISE, CHAN, DUMP>), dim3(grid), dim3(256), 0, st, a);
+    } else if (conv == OFDM_CONV_C) {
+        hipLaunchKernelGGL((rx_ideal_kernel<OFDM_CONV_C, NOISE, CHAN, DUMP>), dim3(grid), dim3(256), 0, st, a);
+    } else {
+        hipLaunchKernelGGL((rx_ideal_kernel<OFDM_CONV_MATLAB, NOISE, CHAN, DUMP>), dim3(grid), dim3(256), 0, st, a);
+    }
+}
+
+template <int NOISE, bool DUMP>
+static void launch_rx_n(hipStream_t st, const RxArgs &a, int est, int conv, int chan, unsigned grid) {
+    if (chan == OFDM_CHAN_AWGN) launch_rx_t<NOISE, OFDM_CHAN_AWGN, DUMP>(st, a, est, conv, grid);
+    else launch_rx_t<NOISE, OFDM_CHAN_RAYLEIGH4, DUMP>(st, a, est, conv, grid);
+}
+
+void launch_rx(hipStream_t st, const RxArgs &a, const ofdm_cfg &cfg, bool dump, unsigned grid) {
+    if (dump) {
+        switch (cfg.noise) {
+            case OFDM_NOISE_REAL: launch_rx_n<OFDM_NOISE_REAL, true>(st, a, cfg.est, cfg.conv, cfg.channel, grid); break;
+            case OFDM_NOISE_COMPLEX: launch_rx_n<OFDM_NOISE_COMPLEX, true>(st, a, cfg.est, cfg.conv, cfg.channel, grid); break;
+            default: launch_rx_n<OFDM_NOISE_NONE, true>(st, a, cfg.est, cfg.conv, cfg.channel, grid); break;
+        }
+    } else {
+        switch (cfg.noise) {
+            case OFDM_NOISE_REAL: launch_rx_n<OFDM_NOISE_REAL, false>(st, a, cfg.est, cfg.conv, cfg.channel, grid); break;
+            case OFDM_NOISE_COMPLEX: launch_rx_n<OFDM_NOISE_COMPLEX, false>(st, a, cfg.est, cfg.conv, cfg.channel, grid); break;
+            default: launch_rx_n<OFDM_NOISE_NONE, false>(st, a, cfg.est, cfg.conv, cfg.channel, grid); break;
+        }
+    }
+}
+
+int rx_grid(const ofdm_cfg &cfg, int64_t n_tiles, int device) {
+    // waves needed: one per tile (LS) or per tile pair (ideal); 4 waves per block
+    const int64_t waves = cfg.est == OFDM_EST_LS ? n_tiles : (n_tiles + 1) / 2;
+    const int64_t need = (waves + 3) / 4;
+    int per_cu = 0, cus = 0;
+    const void *k = cfg.est == OFDM_EST_LS
+        ? reinterpret_cast<const void *>(&rx_ls_kernel<OFDM_NOISE_REAL, OFDM_CHAN_AWGN, false>)
+        : reinterpret_cast<const void *>(&rx_ideal_kernel<OFDM_CONV_C, OFDM_NOISE_REAL, OFDM_CHAN_AWGN, false>);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, 0) != hipSuccess || per_cu < 1) per_cu = 2;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1) cus = 256;
+    const int64_t cap = (int64_t)per_cu * cus;
+    const int64_t g = need < cap ? need : cap;
+    return (int)(g < 1 ? 1 : g);
+}
+
+}  // namespace ofdm

@@ -1,0 +1,220 @@
+"""Host-side engine: one ofdm_ctx per GPU, device buffers from PyTorch (plumbing only).
+
+Mirrors the reference's three hot-path functions (src/OFDM.c):
+    Transmitter()            OFDM.c:467-618   -> Engine.transmitter() / Engine.tx_frames()
+    Transmission_Over_Air()  OFDM.c:635-655   -> Engine.transmission_over_air()
+    Receiver()               OFDM.c:941-1165  -> Engine.receiver() / Engine.rx_frames()
+and main()'s SNR loop (OFDM.c:1187-1222) -> Engine.symbol_sweep() / Engine.frame_sweep().
+All arithmetic happens in the HIP kernels of libofdm_mi355x.so.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import abi
+from .abi import Cfg, RxOpts, check, load_library, make_cfg, make_rx_opts
+
+
+def _torch():
+    import torch  # noqa: PLC0415  (device memory / streams only)
+    return torch
+
+
+def _ptr(t) -> C.c_void_p:
+    return C.c_void_p(t.data_ptr())
+
+
+class Engine:
+    """A context bound to one MI355X (gfx950).  Use as a context manager or call close()."""
+
+    def __init__(self, device: int = 0, use_torch_stream: bool = True):
+        self.lib = load_library()
+        self.device = device
+        torch = _torch()
+        if not torch.cuda.is_available():
+            raise abi.OfdmError("no GPU visible: the OFDM engine runs only on gfx950")
+        torch.cuda.set_device(device)
+        h = C.c_void_p()
+        check(self.lib, self.lib.ofdm_ctx_create(device, C.byref(h)), "ofdm_ctx_create")
+        self.ctx = h
+        if use_torch_stream:
+            self.set_stream(torch.cuda.current_stream(device).cuda_stream)
+
+    # ---- lifecycle -------------------------------------------------------------------
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.lib.ofdm_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream_handle: int | None):
+        check(self.lib, self.lib.ofdm_ctx_set_stream(self.ctx, C.c_void_p(stream_handle or 0)), "set_stream")
+
+    def synchronize(self):
+        check(self.lib, self.lib.ofdm_ctx_synchronize(self.ctx), "synchronize")
+
+    # ---- timing ----------------------------------------------------------------------
+    def timing(self, enable: bool = True):
+        check(self.lib, self.lib.ofdm_timing_enable(self.ctx, int(enable)), "timing_enable")
+
+    def timing_reset(self):
+        check(self.lib, self.lib.ofdm_timing_reset(self.ctx), "timing_reset")
+
+    def timing_query(self, kernel: int) -> tuple[float, int]:
+        ms = C.c_double(); n = C.c_int64()
+        check(self.lib, self.lib.ofdm_timing_query(self.ctx, kernel, C.byref(ms), C.byref(n)), "timing_query")
+        return ms.value, n.value
+
+    # ---- K1: batched 64-point transforms (device tensors, complex64 [n, 64]) -----------
+    def fft64(self, x, inverse: bool = False, conv: str = "c"):
+        torch = _torch()
+        x = x.contiguous()
+        assert x.dtype == torch.complex64 and x.shape[-1] == 64 and x.is_cuda
+        out = torch.empty_like(x)
+        n = x.numel() // 64
+        check(self.lib, self.lib.ofdm_fft64(self.ctx, _ptr(x), _ptr(out), n, int(inverse), abi.CONV[conv]), "fft64")
+        return out
+
+    # ---- symbol mode (the per-symbol chain) ---------------------------------------------
+    def tx_buffers(self, n_frames: int):
+        torch = _torch()
+        tb = C.c_int64(); bb = C.c_int64()
+        check(self.lib, self.lib.ofdm_tx_bytes(n_frames, C.byref(tb), C.byref(bb)), "tx_bytes")
+        tx = torch.empty(tb.value // 8, dtype=torch.complex64, device=f"cuda:{self.device}")
+        bits = torch.empty(bb.value // 4, dtype=torch.int32, device=f"cuda:{self.device}")
+        return tx, bits
+
+    def tx_frames(self, cfg: Cfg, first_frame: int, n_frames: int, tx=None, bits=None):
+        if tx is None or bits is None:
+            tx, bits = self.tx_buffers(n_frames)
+        check(self.lib, self.lib.ofdm_tx_frames(self.ctx, C.byref(cfg), first_frame, n_frames, _ptr(tx), _ptr(bits)),
+              "tx_frames")
+        return tx, bits
+
+    def new_counters(self, n_snr: int):
+        torch = _torch()
+        return torch.zeros((n_snr, abi.NCOUNTERS), dtype=torch.int64, device=f"cuda:{self.device}")
+
+    def rx_frames(self, cfg: Cfg, tx, bits, first_frame: int, n_frames: int, snr_db, counters=None):
+        snr = np.ascontiguousarray(snr_db, np.float64)
+        if counters is None:
+            counters = self.new_counters(len(snr))
+        check(self.lib, self.lib.ofdm_rx_frames(self.ctx, C.byref(cfg), _ptr(tx), _ptr(bits), first_frame, n_frames,
+                                                snr.ctypes.data_as(C.c_void_p), len(snr), _ptr(counters)), "rx_frames")
+        return counters
+
+    def rx_frames_dump(self, cfg: Cfg, tx, bits, first_frame: int, n_frames: int, snr_db):
+        torch = _torch()
+        snr = np.ascontiguousarray(snr_db, np.float64)
+        counters = self.new_counters(len(snr))
+        eq = torch.zeros((len(snr), n_frames, 2, 48), dtype=torch.complex64, device=f"cuda:{self.device}")
+        db = torch.zeros((len(snr), n_frames, 2, 3), dtype=torch.int32, device=f"cuda:{self.device}")
+        check(self.lib, self.lib.ofdm_rx_frames_dump(self.ctx, C.byref(cfg), _ptr(tx), _ptr(bits), first_frame,
+                                                     n_frames, snr.ctypes.data_as(C.c_void_p), len(snr),
+                                                     _ptr(counters), _ptr(eq), _ptr(db)), "rx_frames_dump")
+        return counters, eq, db
+
+    def symbol_sweep(self, cfg: Cfg, snr_db, n_frames: int, first_frame: int = 0, chunk_frames: int = 0) -> np.ndarray:
+        snr = np.ascontiguousarray(snr_db, np.float64)
+        out = np.zeros((len(snr), abi.NCOUNTERS), np.int64)
+        check(self.lib, self.lib.ofdm_symbol_sweep(self.ctx, C.byref(cfg), snr.ctypes.data_as(C.c_void_p), len(snr),
+                                                   first_frame, n_frames, chunk_frames,
+                                                   out.ctypes.data_as(C.c_void_p)), "symbol_sweep")
+        return out
+
+    # ---- frame mode (the reference's own trial) -----------------------------------------
+    def transmitter(self, conv: str = "c", payload: str = "message", float_taps: bool = True) -> np.ndarray:
+        cap = 20000
+        buf = np.zeros(2 * cap, np.float32)
+        n = C.c_int32()
+        check(self.lib, self.lib.ofdm_transmitter(self.ctx, abi.CONV[conv], abi.PAYLOAD[payload], int(float_taps),
+                                                  buf.ctypes.data_as(C.c_void_p), cap, C.byref(n)), "transmitter")
+        return buf[:2 * n.value].view(np.complex64).copy()
+
+    def transmission_over_air(self, tx: np.ndarray, snr_db: float, seed: int = 0x80211A, trial: int = 0,
+                              snr_index: int = 0) -> np.ndarray:
+        tx = np.ascontiguousarray(tx, np.complex64)
+        out = np.zeros_like(tx)
+        check(self.lib, self.lib.ofdm_transmission_over_air(self.ctx, tx.ctypes.data_as(C.c_void_p),
+                                                            out.ctypes.data_as(C.c_void_p), len(tx), snr_db, seed,
+                                                            trial, snr_index), "transmission_over_air")
+        return out
+
+    def receiver(self, capture: np.ndarray, mode: str = "c", payload: str = "message"):
+        opts = make_rx_opts(mode)
+        cap = np.ascontiguousarray(capture[:opts.cap_len], np.complex64)
+        if len(cap) != opts.cap_len:
+            raise ValueError(f"capture must hold {opts.cap_len} samples")
+        res = np.zeros(3, np.float32); ints = np.zeros(4, np.int32)
+        bits = np.zeros(192, np.int32); eq = np.zeros(2 * 96, np.float32)
+        check(self.lib, self.lib.ofdm_receiver(self.ctx, cap.ctypes.data_as(C.c_void_p), C.byref(opts),
+                                               abi.PAYLOAD[payload], res.ctypes.data_as(C.c_void_p),
+                                               ints.ctypes.data_as(C.c_void_p), bits.ctypes.data_as(C.c_void_p),
+                                               eq.ctypes.data_as(C.c_void_p)), "receiver")
+        return dict(res=res, packet_idx=int(ints[0]), sync_fail=int(ints[1]), oob=int(ints[2]), bits=bits,
+                    eq=eq.view(np.complex64).copy())
+
+    def frame_sweep(self, cfg: Cfg, snr_db, n_trials: int, first_trial: int = 0, mode: str = "c",
+                    fixed_start: int = -1, want_packet_idx: bool = False):
+        snr = np.ascontiguousarray(snr_db, np.float64)
+        out = np.zeros((len(snr), abi.NCOUNTERS), np.int64)
+        pidx = np.zeros((len(snr), n_trials), np.int32) if want_packet_idx else None
+        opts = make_rx_opts(mode, fixed_start)
+        check(self.lib, self.lib.ofdm_frame_sweep(self.ctx, C.byref(cfg), C.byref(opts), snr.ctypes.data_as(C.c_void_p),
+                                                  len(snr), first_trial, n_trials, out.ctypes.data_as(C.c_void_p),
+                                                  None if pidx is None else pidx.ctypes.data_as(C.c_void_p)),
+              "frame_sweep")
+        return (out, pidx) if want_packet_idx else out
+
+
+@dataclass
+class SweepResult:
+    snr_db: np.ndarray
+    counters: np.ndarray
+
+    @property
+    def ber(self) -> np.ndarray:
+        c = self.counters
+        return c[:, abi.C_BIT_ERR] / np.maximum(c[:, abi.C_BITS], 1)
+
+    @property
+    def evm_pre_db(self) -> np.ndarray:
+        """pooled EVM before the slicer: 10 log10(sum|z-d|^2 / sum|d|^2) (OFDM.c:1104-1126)"""
+        c = self.counters
+        with np.errstate(divide="ignore"):
+            return 10 * np.log10(c[:, abi.C_EVM_PRE_Q] / abi.EVM_Q_SCALE / np.maximum(c[:, abi.C_EVM_TERMS], 1))
+
+    @property
+    def evm_post_db(self) -> np.ndarray:
+        """pooled EVM after the slicer (OFDM.c:1128-1150); -inf when no slicer error"""
+        c = self.counters
+        with np.errstate(divide="ignore"):
+            return 10 * np.log10(2.0 * c[:, abi.C_EVM_POST_AXIS] / np.maximum(c[:, abi.C_EVM_TERMS], 1))
+
+    @property
+    def mean_frame_evm_db(self) -> np.ndarray:
+        """mean over frames of the per-frame EVM_dB the reference prints per trial (OFDM.c:1126)"""
+        c = self.counters
+        return c[:, abi.C_EVMDB_PRE_Q] / abi.EVM_Q_SCALE / np.maximum(c[:, abi.C_FRAMES], 1)
+
+    @property
+    def sync_fail_rate(self) -> np.ndarray:
+        c = self.counters
+        return c[:, abi.C_SYNC_FAIL] / np.maximum(c[:, abi.C_FRAMES], 1)
+
+
+__all__ = ["Engine", "SweepResult", "make_cfg", "make_rx_opts"]
