@@ -99,6 +99,13 @@ def load_library(path: Path | str | None = None) -> C.CDLL:
     if _LIB is not None and path is None:
         return _LIB
     p = Path(path or LIB_PATH)
+    try:
+        # PyTorch ships its own libamdhip64 (same SONAME).  Loading it first makes this library
+        # bind to that one HIP runtime instead of starting a second one from /opt/rocm, which
+        # would then see no device.
+        import torch  # noqa: F401,PLC0415
+    except ImportError:
+        pass
     if not p.exists():
         raise OfdmError(f"{p} not found: the HIP library must be built (build_lib.build()); "
                         "there is no CPU fallback")

@@ -12,6 +12,7 @@
 // each sub-block's bins are consumed (demapped or stored) at once.  sched_fence() pins that
 // order so the live set stays ~128 VGPRs + temporaries (3 waves/SIMD, no scratch).
 #include "ofdm_internal.h"
+#include "ofdm_rxcommon.h"
 
 #ifndef OFDM_RX_WAVES_PER_SIMD
 #define OFDM_RX_WAVES_PER_SIMD 2
@@ -220,131 +221,6 @@ __device__ __forceinline__ void rx_window_stage1(float2 (&x)[64], const WindowSr
         static_for<0, 4>([&](auto ic) { dif_stage1<false, 4 * g + decltype(ic)::value>(x); });
         sched_fence();
     });
-}
-
-template <int CTRL>
-__device__ __forceinline__ float dpp_f(float v) {
-    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
-}
-template <int CTRL>
-__device__ __forceinline__ float2 dpp_c(float2 v) { return make_float2(dpp_f<CTRL>(v.x), dpp_f<CTRL>(v.y)); }
-constexpr int DPP_QUAD_BCAST0 = 0x00;   // quad_perm [0,0,0,0]
-constexpr int DPP_QUAD_BCAST1 = 0x55;   // quad_perm [1,1,1,1]
-
-__device__ __forceinline__ void channel_taps(uint32_t f_lo, uint32_t f_hi, uint32_t k0, uint32_t k1, float2 (&h)[4]) {
-    const Gauss4 a = gauss4(f_lo, f_hi, 0u, STREAM_CHAN, k0, k1);
-    const Gauss4 b = gauss4(f_lo, f_hi, 1u, STREAM_CHAN, k0, k1);
-    const float s = 0.35355339059327376220f;   // sqrt(1/8): CN(0, 1/4) per tap
-    h[0] = make_float2(s * a.z[0], s * a.z[1]);
-    h[1] = make_float2(s * a.z[2], s * a.z[3]);
-    h[2] = make_float2(s * b.z[0], s * b.z[1]);
-    h[3] = make_float2(s * b.z[2], s * b.z[3]);
-}
-
-// Per-symbol decisions + metrics, consumed one FFT sub-block at a time.
-//   Z = Y / H (OFDM.c:1044-1052), slicer (OFDM.c:852-871), demap (OFDM.c:873-908), bit compare
-//   (OFDM.c:1154-1161), EVM pre/post (OFDM.c:1104-1150).
-struct SymState { float evm_pre; uint32_t d[3]; };
-
-template <bool DUMP, int R, typename HF>
-__device__ __forceinline__ void demap_sub(const float2 (&x)[64], const uint32_t (&wi)[3], HF &&Hof, float2 *dump_eq,
-                                          SymState &st) {
-    uint32_t w[3] = {wi[0], wi[1], wi[2]};
-    opaque(w[0]); opaque(w[1]); opaque(w[2]);     // truth selects are made here, not hoisted
-    static_for<0, 16>([&](auto kc) {
-        constexpr int bin = 4 * decltype(kc)::value + R;
-        constexpr int m = data_index(bin);
-        if constexpr (m >= 0) {
-            const float2 z = Hof(x[digit_rev4(bin)], std::integral_constant<int, bin>{});
-            if constexpr (DUMP) { if (dump_eq) dump_eq[m] = z; }
-            const uint32_t pr = z.x > 0.f, pi = z.y > 0.f;
-            constexpr int s0 = 31 - ((2 * m) & 31), s1 = 31 - ((2 * m + 1) & 31), wi = (2 * m) >> 5;
-            st.d[wi] |= ((pi ^ 1u) << s0) | ((pr ^ pi) << s1);
-            const uint32_t b0 = bit_of(w, 2 * m), b1 = bit_of(w, 2 * m + 1);
-            const float dr = (b0 == b1) ? INV_SQRT2 : -INV_SQRT2;
-            const float di = b0 ? -INV_SQRT2 : INV_SQRT2;
-            const float ex = z.x - dr, ey = z.y - di;
-            st.evm_pre = fmaf(ex, ex, fmaf(ey, ey, st.evm_pre));
-        }
-    });
-}
-
-__device__ __forceinline__ void symbol_errors(const SymState &st, const uint32_t (&w)[3], uint32_t &be, uint32_t &ax) {
-    be = 0; ax = 0;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const uint32_t e = st.d[i] ^ w[i];
-        const uint32_t e0 = e & 0xAAAAAAAAu, e1 = e & 0x55555555u;   // b0 (imag axis) / b1 positions
-        be += __popc(e);
-        ax += __popc(e0) + __popc((e0 >> 1) ^ e1);                     // im wrong + (re xor im) wrong
-    }
-}
-
-// frame-level counters of one wave, reduced and added into the block's LDS slots
-struct FrameAcc {
-    uint32_t bit_err = 0, frame_err = 0, axis = 0, post_finite = 0;
-    int64_t pre_q = 0, dbpre_q = 0, dbpost_q = 0;
-};
-
-__device__ __forceinline__ void frame_metrics(FrameAcc &acc, float fe_pre, uint32_t ferr, uint32_t fax) {
-    const float N = 96.0f;   // 48 subcarriers x D = 2
-    acc.bit_err += ferr;
-    acc.frame_err += ferr > 0u;
-    acc.axis += fax;
-    acc.pre_q += (int64_t)__float2ll_rn(fe_pre * (float)OFDM_EVM_Q_SCALE);
-    // per-frame EVM_dB = 10 log10(sum|e|^2 / sum|d|^2), |d| = 1 (OFDM.c:1124-1126), floor -400 dB
-    const float lg = 3.01029995663981195214f * __builtin_amdgcn_logf(fe_pre / N);   // 10 log10(2) log2
-    const float db = fe_pre > 0.f ? fmaxf(lg, -400.0f) : -400.0f;
-    acc.dbpre_q += (int64_t)__float2ll_rn(db * (float)OFDM_EVM_Q_SCALE);
-    if (fax > 0u) {
-        const float dbp = 3.01029995663981195214f * __builtin_amdgcn_logf(2.0f * (float)fax / N);
-        acc.dbpost_q += (int64_t)__float2ll_rn(dbp * (float)OFDM_EVM_Q_SCALE);
-        acc.post_finite += 1u;
-    }
-}
-
-
-__device__ __forceinline__ void flush_wave(const FrameAcc &acc, unsigned long long *slots /*[8]*/) {
-    // per wave and SNR: bit_err, axis <= 32 frames x 192 < 2^16; frame counts <= 32
-    const uint32_t p0 = wave_sum_u32(acc.bit_err | (acc.axis << 16));
-    const uint32_t p1 = wave_sum_u32(acc.frame_err | (acc.post_finite << 16));
-    const uint32_t a0 = p0 & 0xFFFFu, a2 = p0 >> 16, a1 = p1 & 0xFFFFu, a3 = p1 >> 16;
-    const uint64_t b0 = wave_sum_u64((uint64_t)acc.pre_q), b1 = wave_sum_u64((uint64_t)acc.dbpre_q);
-    const uint64_t b2 = wave_sum_u64((uint64_t)acc.dbpost_q);
-    if ((threadIdx.x & 63) == 0) {
-        atomicAdd(&slots[0], (unsigned long long)a0);
-        atomicAdd(&slots[1], (unsigned long long)a1);
-        atomicAdd(&slots[2], (unsigned long long)a2);
-        atomicAdd(&slots[3], (unsigned long long)a3);
-        atomicAdd(&slots[4], (unsigned long long)b0);
-        atomicAdd(&slots[5], (unsigned long long)b1);
-        atomicAdd(&slots[6], (unsigned long long)b2);
-    }
-}
-
-// LDS slot k -> counter index
-__device__ __forceinline__ int slot_counter(int k) {
-    return k == 0 ? OFDM_C_BIT_ERR : k == 1 ? OFDM_C_FRAME_ERR : k == 2 ? OFDM_C_EVM_POST_AXIS
-         : k == 3 ? OFDM_C_EVMDB_POST_FINITE : k == 4 ? OFDM_C_EVM_PRE_Q : k == 5 ? OFDM_C_EVMDB_PRE_Q
-         : OFDM_C_EVMDB_POST_Q;
-}
-
-__device__ __forceinline__ void block_flush(const RxArgs &a, unsigned long long (*sacc)[8]) {
-    __syncthreads();
-    for (int i = threadIdx.x; i < a.n_snr * 7; i += blockDim.x) {
-        const int q = i / 7, k = i % 7;
-        const unsigned long long v = sacc[q][k];
-        if (v) atomicAdd(&a.counters[q * OFDM_NCOUNTERS + slot_counter(k)], v);
-    }
-    if (blockIdx.x == 0) {
-        for (int q = threadIdx.x; q < a.n_snr; q += blockDim.x) {
-            unsigned long long *c = a.counters + q * OFDM_NCOUNTERS;
-            atomicAdd(&c[OFDM_C_FRAMES], (unsigned long long)a.n_frames);
-            atomicAdd(&c[OFDM_C_SYMBOLS], (unsigned long long)(2 * a.n_frames));
-            atomicAdd(&c[OFDM_C_BITS], (unsigned long long)(192 * a.n_frames));
-            atomicAdd(&c[OFDM_C_EVM_TERMS], (unsigned long long)(96 * a.n_frames));
-        }
-    }
 }
 
 // Shared tail: FFT sub-blocks + demap, per-frame combine of the two data symbols (quad xor-1
