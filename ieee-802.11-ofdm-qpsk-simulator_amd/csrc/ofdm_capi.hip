@@ -191,7 +191,7 @@ int ofdm_ctx_destroy(ofdm_ctx *ctx) {
 int ofdm_ctx_set_stream(ofdm_ctx *ctx, void *stream) {
     Ctx *c = reinterpret_cast<Ctx *>(ctx);
     if (!c) return set_error(OFDM_E_ARG, "ctx is NULL");
-    c->stream = stream ? reinterpret_cast<hipStream_t>(stream) : c->own;
+    c->stream = reinterpret_cast<hipStream_t>(stream);   // NULL = null stream, ordered with it
     return OFDM_OK;
 }
 

@@ -5,6 +5,24 @@
 
 namespace ofdm {
 
+// Tx subcarrier value of fftshifted bin BIN for a symbol whose payload bits are w (MSB first):
+// QPSK data (OFDM.c:415-433), pilots {1,1,1,-1} (OFDM.c:523-544), nulls/DC 0; times (-1)^BIN for
+// the C ifft convention (D5).
+template <int CONV, int BIN>
+__device__ __forceinline__ float2 tx_bin(const uint32_t (&w)[3]) {
+    constexpr float sgn = (CONV == OFDM_CONV_C && (BIN & 1)) ? -1.0f : 1.0f;   // ifftshift+fftshift (D5)
+    constexpr int m = data_index(BIN);
+    if constexpr (m >= 0) {
+        const uint32_t b0 = bit_of(w, 2 * m), b1 = bit_of(w, 2 * m + 1);
+        // 00:(+,+) 01:(-,+) 10:(-,-) 11:(+,-): re > 0 iff b0 == b1, im > 0 iff b0 == 0 (D10)
+        const float re = (b0 == b1) ? sgn * INV_SQRT2 : -sgn * INV_SQRT2;
+        const float im = b0 ? -sgn * INV_SQRT2 : sgn * INV_SQRT2;
+        return make_float2(re, im);
+    } else {
+        return make_float2(sgn * pilot_at(BIN), 0.0f);    // pilots {1,1,1,-1}; nulls and DC 0
+    }
+}
+
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v) {
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));

@@ -87,21 +87,6 @@ __global__ __launch_bounds__(64, 2) void fft64_kernel(const float2 *__restrict__
 // ======================================================================== K2: Tx builder
 // One lane = one data symbol: bits -> QPSK (OFDM.c:415-433) -> subcarrier map + pilots
 // (OFDM.c:523-548) -> ifft (OFDM.c:320-339, convention D5) -> CP (OFDM.c:559-565) -> HBM.
-template <int CONV, int BIN>
-__device__ __forceinline__ float2 tx_bin(const uint32_t (&w)[3]) {
-    constexpr float sgn = (CONV == OFDM_CONV_C && (BIN & 1)) ? -1.0f : 1.0f;   // ifftshift+fftshift (D5)
-    constexpr int m = data_index(BIN);
-    if constexpr (m >= 0) {
-        const uint32_t b0 = bit_of(w, 2 * m), b1 = bit_of(w, 2 * m + 1);
-        // 00:(+,+) 01:(-,+) 10:(-,-) 11:(+,-): re > 0 iff b0 == b1, im > 0 iff b0 == 0 (D10)
-        const float re = (b0 == b1) ? sgn * INV_SQRT2 : -sgn * INV_SQRT2;
-        const float im = b0 ? -sgn * INV_SQRT2 : sgn * INV_SQRT2;
-        return make_float2(re, im);
-    } else {
-        return make_float2(sgn * pilot_at(BIN), 0.0f);    // pilots {1,1,1,-1}; nulls and DC 0
-    }
-}
-
 template <int CONV>
 __global__ __launch_bounds__(256, 3) void tx_symbols_kernel(TxArgs a) {
     const int64_t sidx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // symbol within batch

@@ -62,7 +62,8 @@ class Engine:
             pass
 
     def set_stream(self, stream_handle: int | None):
-        check(self.lib, self.lib.ofdm_ctx_set_stream(self.ctx, C.c_void_p(stream_handle or 0)), "set_stream")
+        """Enqueue on this hipStream_t handle (0 / None = the null stream, PyTorch's default)."""
+        check(self.lib, self.lib.ofdm_ctx_set_stream(self.ctx, C.c_void_p(stream_handle or None)), "set_stream")
 
     def synchronize(self):
         check(self.lib, self.lib.ofdm_ctx_synchronize(self.ctx), "synchronize")

@@ -91,7 +91,8 @@ const char *ofdm_last_error(void);
 int ofdm_device_count(int *count);
 int ofdm_ctx_create(int device, ofdm_ctx **out);
 int ofdm_ctx_destroy(ofdm_ctx *ctx);
-/* run all work of this context on an external hipStream_t (e.g. torch's current stream); NULL = own stream */
+/* Enqueue all work of this context on hip_stream from now on (e.g. PyTorch's current stream).
+ * NULL selects the HIP null (default) stream.  A new context uses its own non-blocking stream. */
 int ofdm_ctx_set_stream(ofdm_ctx *ctx, void *hip_stream);
 int ofdm_ctx_synchronize(ofdm_ctx *ctx);
 /* kernel timing: when enabled, every launch of the named kernel is bracketed by HIP events on the

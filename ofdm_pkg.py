@@ -30,4 +30,12 @@ def build(force: bool = False):
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv))
+    # python ofdm_pkg.py build [--force]      compile libofdm_mi355x.so
+    # python ofdm_pkg.py sweep [args...]      OFDM.c main() on the GPU (see ofdm_amd.sweep)
+    cmd = sys.argv[1] if len(sys.argv) > 1 else "build"
+    if cmd == "sweep":
+        load()
+        from ofdm_amd import sweep  # noqa: PLC0415
+        sweep.main(sys.argv[2:])
+    else:
+        print(build(force="--force" in sys.argv))
