@@ -50,8 +50,9 @@ __device__ __forceinline__ uint4 philox10(uint32_t c0, uint32_t c1, uint32_t c2,
     for (int r = 0; r < 10; ++r) {
         const uint64_t p0 = (uint64_t)PHILOX_M0 * c0;   // v_mad_u64_u32
         const uint64_t p1 = (uint64_t)PHILOX_M1 * c2;
-        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
-        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        // 3-input XOR in one v_bitop3_b32 (truth table 0x96), key words from SGPRs
+        const uint32_t n0 = __builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c1, k0, 0x96);
+        const uint32_t n2 = __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c3, k1, 0x96);
         c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
         k0 += PHILOX_W0; k1 += PHILOX_W1;
     }

@@ -361,11 +361,11 @@ __global__ __launch_bounds__(64) void frame_rx_kernel(FrameArgs a) {
         float2 *deq = dump ? a.dbg_eq + 48 * (role - 2) : nullptr;
         auto Hof = [&](float2 Y, auto binc) {
             constexpr int bin = decltype(binc)::value;
-            constexpr float hs = 0.5f * (float)ltf_sign(bin);
+            constexpr float hs = 2.0f * (float)ltf_sign(bin);    // Y / (0.5 Lf S) = Y conj(S) 2 Lf / |S|^2
             const float2 F1 = dpp_c<0x00>(Y), F2 = dpp_c<0x55>(Y);
-            const float2 H = make_float2(hs * (F1.x + F2.x), hs * (F1.y + F2.y));
-            const float inv = __builtin_amdgcn_rcpf(fmaf(H.x, H.x, H.y * H.y));
-            return cscale(cmulc(Y, H), inv);
+            const float2 S = make_float2(F1.x + F2.x, F1.y + F2.y);
+            const float inv = hs * __builtin_amdgcn_rcpf(fmaf(S.x, S.x, S.y * S.y));
+            return cscale(cmulc(Y, S), inv);
         };
         static_for<0, 4>([&](auto rc) { demap_sub<true, decltype(rc)::value>(x, w, Hof, deq, st); });
         uint32_t be, ax;

@@ -290,11 +290,12 @@ __global__ __launch_bounds__(256, OFDM_RX_WAVES_PER_SIMD) void rx_ls_kernel(RxAr
             // H[k] = 0.5 (F1[k] + F2[k]) conj(Lf[k]), Lf = +-1 on data bins (OFDM.c:846-849)
             auto Hof = [&](float2 Y, auto binc) {
                 constexpr int bin = decltype(binc)::value;
-                constexpr float hs = 0.5f * (float)ltf_sign(bin);
+                // with S = F1 + F2 and H = 0.5 Lf S (Lf = +-1): Y / H = Y conj(S) * (2 Lf / |S|^2)
+                constexpr float hs = 2.0f * (float)ltf_sign(bin);
                 const float2 F1 = dpp_c<DPP_QUAD_BCAST0>(Y), F2 = dpp_c<DPP_QUAD_BCAST1>(Y);
-                const float2 H = make_float2(hs * (F1.x + F2.x), hs * (F1.y + F2.y));
-                const float inv = __builtin_amdgcn_rcpf(fmaf(H.x, H.x, H.y * H.y));
-                return cscale(cmulc(Y, H), inv);
+                const float2 S = make_float2(F1.x + F2.x, F1.y + F2.y);
+                const float inv = hs * __builtin_amdgcn_rcpf(fmaf(S.x, S.x, S.y * S.y));
+                return cscale(cmulc(Y, S), inv);
             };
             finish_symbol<DUMP>(x, wq, Hof, dump_eq, dump_bits, role == 2 && valid, sacc[q]);
         }
