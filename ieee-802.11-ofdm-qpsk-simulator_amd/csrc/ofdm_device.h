@@ -164,6 +164,10 @@ typedef __attribute__((address_space(1))) const f2v gcf2;
 typedef __attribute__((address_space(1))) f2v gf2;
 __device__ __forceinline__ float2 gld(gcf2 *p, int i) { const f2v v = p[i]; return make_float2(v.x, v.y); }
 __device__ __forceinline__ void gst(gf2 *p, int i, float2 v) { f2v t; t.x = v.x; t.y = v.y; p[i] = t; }
+// LDS views (address space 3)
+typedef __attribute__((address_space(3))) const f2v lcf2;
+__device__ __forceinline__ float2 ld2(gcf2 *p, int i) { return gld(p, i); }
+__device__ __forceinline__ float2 ld2(lcf2 *p, int i) { const f2v v = p[i]; return make_float2(v.x, v.y); }
 
 // ------------------------------------------------------------------ wave64 reductions via DPP
 template <int CTRL>

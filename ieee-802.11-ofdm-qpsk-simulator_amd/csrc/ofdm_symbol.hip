@@ -135,25 +135,28 @@ __global__ __launch_bounds__(256, 3) void tx_symbols_kernel(TxArgs a) {
 // ======================================================================== K3: receiver chain
 // Clean sample n of a window: data windows read row 16+n of the Tx tile (n >= -3 reaches into the
 // CP), LTF windows read the cyclic training symbol T[(n + 64) & 63].
+// P is a global (gcf2) or LDS (lcf2) view.
+template <typename P>
 struct WindowSrc {
-    gcf2 *p;             // data: &tile[16][slot]; LTF: T
+    P *p;                // data: &tile[16][slot]; LTF: T
     int stride;          // 32 (data) or 1 (LTF)
     bool circ;           // LTF
 };
-__device__ __forceinline__ float2 src_at(gcf2 *p, int stride, bool circ, int n) {
-    if (n >= 0) return gld(p, n * stride);
-    return circ ? gld(p, 64 + n) : gld(p, n * stride);
+template <typename P>
+__device__ __forceinline__ float2 src_at(P *p, int stride, bool circ, int n) {
+    if (n >= 0) return ld2(p, n * stride);
+    return circ ? ld2(p, 64 + n) : ld2(p, n * stride);
 }
 
 // Load + channel + AWGN for samples n0..n0+3, times (-1)^n (fft() = DFT of x(-1)^n, OFDM.c:314-318).
 // Noise sample at frame time t uses Gaussian t (real) or 2t, 2t+1 (complex) of the frame's stream
 // (DESIGN.md §3); AWGN is real-only as OFDM.c:651 really does (D7).
-template <int NOISE, int CHAN, int N0>
-__device__ __forceinline__ void rx_block(float2 (&x)[64], const WindowSrc &src, uint32_t f_lo, uint32_t f_hi,
+template <int NOISE, int CHAN, int N0, typename WS>
+__device__ __forceinline__ void rx_block(float2 (&x)[64], const WS &src, uint32_t f_lo, uint32_t f_hi,
                                          uint32_t t0, uint32_t q, float sigma, uint32_t k0, uint32_t k1,
                                          const float2 (&h)[4]) {
     // re-materialise per block: keeps LICM from hoisting 16 blocks' worth of addresses / round-1 products
-    gcf2 *p = src.p;
+    auto p = src.p;
     uint32_t flo = f_lo, fhi = f_hi, tb = t0;
     opaque(p); opaque(flo); opaque(fhi); opaque(tb);
     f_lo = flo; f_hi = fhi; t0 = tb;
@@ -193,8 +196,8 @@ __device__ __forceinline__ void rx_block(float2 (&x)[64], const WindowSrc &src, 
 }
 
 // generate the window fused with the first radix-4 stage (4 butterflies per group)
-template <int NOISE, int CHAN>
-__device__ __forceinline__ void rx_window_stage1(float2 (&x)[64], const WindowSrc &src, uint32_t f_lo,
+template <int NOISE, int CHAN, typename WS>
+__device__ __forceinline__ void rx_window_stage1(float2 (&x)[64], const WS &src, uint32_t f_lo,
                                                  uint32_t f_hi, uint32_t t0, uint32_t q, float sigma,
                                                  uint32_t k0, uint32_t k1, const float2 (&h)[4]) {
     static_for<0, 4>([&](auto gc) {
@@ -236,27 +239,56 @@ __device__ __forceinline__ void finish_symbol(float2 (&x)[64], const uint32_t (&
 }
 
 // ---- LS estimate: quad = {LTF1, LTF2, D0, D1} of one frame; wave = 16 frames = one tile ----
+// Each wave stages the rows of its tile the windows read (16..79, or 12..79 when the 4-tap channel
+// reaches 3 samples into the CP) into its own LDS slice once, with global_load_lds_dwordx4 (1 KB per
+// wave instruction), so the n_snr passes over the tile read LDS instead of re-fetching HBM/L2.
+template <int CHAN>
+struct LsStage {
+    static constexpr int R0 = CHAN == OFDM_CHAN_RAYLEIGH4 ? 12 : 16;
+    static constexpr int ROWS = SYM_SAMPLES - R0;
+    static constexpr int BYTES = ROWS * TILE_SYMBOLS * 8;
+    static constexpr int CHUNKS = BYTES / 1024;
+    static_assert(BYTES % 1024 == 0, "staged rows must be whole 1 KB wave chunks");
+};
+
 template <int NOISE, int CHAN, bool DUMP>
 __global__ __launch_bounds__(256, OFDM_RX_WAVES_PER_SIMD) void rx_ls_kernel(RxArgs a) {
+    using St = LsStage<CHAN>;
     __shared__ unsigned long long sacc[OFDM_MAX_SNR][8];
+    __shared__ __attribute__((aligned(16))) float2 s_tile[4][St::ROWS * TILE_SYMBOLS];
+    __shared__ float2 s_ltf[64];
     for (int i = threadIdx.x; i < a.n_snr * 8; i += blockDim.x) (&sacc[0][0])[i] = 0ull;
+    if (threadIdx.x < 64) s_ltf[threadIdx.x] = a.ltf[threadIdx.x];
     __syncthreads();
     const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
     const int role = lane & 3, fi = lane >> 2;
-    const int64_t wave_id = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t wave_id = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
     const int64_t n_waves = (int64_t)gridDim.x * (blockDim.x >> 6);
     // window start on the frame timeline: LTF1 192, LTF2 256, D0 336, D1 416
     const uint32_t t0 = role == 0 ? 192u : role == 1 ? 256u : (role == 2 ? 336u : 416u);
     const bool is_data = role >= 2;
     const int slot = 2 * fi + (role & 1);
+    float2 *my_tile = s_tile[wv];
 
     for (int64_t tile = wave_id; tile < a.n_tiles; tile += n_waves) {
         const int64_t fl = tile * TILE_FRAMES + fi;
         const bool valid = fl < a.n_frames;
         const uint64_t f = a.first_frame + (uint64_t)fl;
         const uint32_t f_lo = (uint32_t)f, f_hi = (uint32_t)(f >> 32);
-        WindowSrc src;
-        src.p = (gcf2 *)(is_data ? a.tx + tile * (SYM_SAMPLES * TILE_SYMBOLS) + 16 * TILE_SYMBOLS + slot : a.ltf);
+        {
+            // previous tile's LDS reads were consumed by its FFTs, so the slice is free to overwrite
+            const char *g = (const char *)(a.tx + tile * (SYM_SAMPLES * TILE_SYMBOLS) + St::R0 * TILE_SYMBOLS) + lane * 16;
+            static_for<0, St::CHUNKS>([&](auto cc) {
+                constexpr int c = decltype(cc)::value;
+                __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(g + c * 1024),
+                                                 (__attribute__((address_space(3))) void *)((char *)my_tile + c * 1024),
+                                                 16, 0, 0);
+            });
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        WindowSrc<lcf2> src;
+        src.p = is_data ? (lcf2 *)(my_tile + (16 - St::R0) * TILE_SYMBOLS + slot) : (lcf2 *)s_ltf;
         src.stride = is_data ? TILE_SYMBOLS : 1;
         src.circ = !is_data;
         uint32_t w[3] = {0u, 0u, 0u};
@@ -268,7 +300,7 @@ __global__ __launch_bounds__(256, OFDM_RX_WAVES_PER_SIMD) void rx_ls_kernel(RxAr
         if constexpr (CHAN == OFDM_CHAN_RAYLEIGH4) channel_taps(f_lo, f_hi, a.k0, a.k1, h);
 
         for (int q = 0; q < a.n_snr; ++q) {
-            WindowSrc s = src;
+            WindowSrc<lcf2> s = src;
             uint32_t wq[3] = {w[0], w[1], w[2]};
             uint32_t flo = f_lo, fhi = f_hi;
             float2 hq[4] = {h[0], h[1], h[2], h[3]};
@@ -322,7 +354,7 @@ __global__ __launch_bounds__(256, OFDM_RX_WAVES_PER_SIMD) void rx_ideal_kernel(R
         const bool valid = fl < a.n_frames;
         const uint64_t f = a.first_frame + (uint64_t)fl;
         const uint32_t f_lo = (uint32_t)f, f_hi = (uint32_t)(f >> 32);
-        WindowSrc src;
+        WindowSrc<gcf2> src;
         src.p = (gcf2 *)(a.tx + tile * (SYM_SAMPLES * TILE_SYMBOLS) + 16 * TILE_SYMBOLS + slot);
         src.stride = TILE_SYMBOLS;
         src.circ = false;
@@ -331,7 +363,7 @@ __global__ __launch_bounds__(256, OFDM_RX_WAVES_PER_SIMD) void rx_ideal_kernel(R
         float2 h[4] = {make_float2(1.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f)};
         if constexpr (CHAN == OFDM_CHAN_RAYLEIGH4) channel_taps(f_lo, f_hi, a.k0, a.k1, h);
         for (int q = 0; q < a.n_snr; ++q) {
-            WindowSrc s = src;
+            WindowSrc<gcf2> s = src;
             uint32_t wq[3] = {w[0], w[1], w[2]};
             uint32_t flo = f_lo, fhi = f_hi;
             float2 hq[4] = {h[0], h[1], h[2], h[3]};
