@@ -355,25 +355,17 @@ __global__ __launch_bounds__(64) void frame_rx_kernel(FrameArgs a) {
         fft64<false>(x);
         const uint32_t w[3] = {a.table[3 * (role & 1)], a.table[3 * (role & 1) + 1], a.table[3 * (role & 1) + 2]};
         SymState st;
-        st.evm_pre = 0.f;
-        st.d[0] = st.d[1] = st.d[2] = 0u;
+        sym_init(st);
         const bool dump = a.dbg_eq && it == 0 && lane < 4 && role >= 2;
         float2 *deq = dump ? a.dbg_eq + 48 * (role - 2) : nullptr;
-        auto Hof = [&](float2 Y, auto binc) {
-            constexpr int bin = decltype(binc)::value;
-            constexpr float hs = 2.0f * (float)ltf_sign(bin);    // Y / (0.5 Lf S) = Y conj(S) 2 Lf / |S|^2
-            const float2 F1 = dpp_c<0x00>(Y), F2 = dpp_c<0x55>(Y);
-            const float2 S = make_float2(F1.x + F2.x, F1.y + F2.y);
-            const float inv = hs * __builtin_amdgcn_rcpf(fmaf(S.x, S.x, S.y * S.y));
-            return cscale(cmulc(Y, S), inv);
-        };
-        static_for<0, 4>([&](auto rc) { demap_sub<true, decltype(rc)::value>(x, w, Hof, deq, st); });
-        uint32_t be, ax;
-        symbol_errors(st, w, be, ax);
-        const float e_other = dpp_f<0xB1>(st.evm_pre);
+        auto Hof = [&](float2 Y, auto binc) { return ls_equalise<decltype(binc)::value>(Y); };
+        static_for<0, 4>([&](auto rc) { demap_sub<true, decltype(rc)::value, 2>(x, w, Hof, deq, st); });
+        const uint32_t be = st.be, ax = st.ax;
+        const float evm = finish_evm<2>(st);
+        const float e_other = dpp_f<0xB1>(evm);
         const uint32_t be_other = dpp_u<0xB1>(be), ax_other = dpp_u<0xB1>(ax);
         if (lane == 2) {
-            const float fe = st.evm_pre + e_other;
+            const float fe = evm + e_other;
             const uint32_t ferr = be + be_other, fax = ax + ax_other;
             unsigned long long *s = acc[q];
             s[0] += ferr;

@@ -45,40 +45,94 @@ __device__ __forceinline__ void channel_taps(uint32_t f_lo, uint32_t f_hi, uint3
 // Per-symbol decisions + metrics, consumed one FFT sub-block at a time.
 //   Z = Y / H (OFDM.c:1044-1052), slicer (OFDM.c:852-871), demap (OFDM.c:873-908), bit compare
 //   (OFDM.c:1154-1161), EVM pre/post (OFDM.c:1104-1150).
-struct SymState { float evm_pre; uint32_t d[3]; };
+//
+// The equaliser hands back Z = u * g with g > 0, so the slicer decision is the sign of u:
+//   KIND 0: g = 1 (ideal AWGN), KIND 1: g = r (ideal ZF, r = 1/|H|^2),
+//   KIND 2: g = 2 r (LTF LS: Y / (0.5 Lf S) = 2 Lf Y conj(S) / |S|^2, r = 1/|S|^2).
+// With the truth symbol d = (sr c, si c), c = 1/sqrt2 (non-Gray map, D10: re < 0 iff b0 != b1,
+// im < 0 iff b0), flipping u's sign bits by (sr, si) gives u' with
+//   |Z - d|^2 = (u'.x g - c)^2 + (u'.y g - c)^2     and     axis error <=> sign bit of u' set,
+// so each bin costs one bitop3 per axis for the truth, one fma per axis for the EVM and one
+// alignbit per axis to collect the errors (popcounted once per sub-block).  Decisions agree with
+// "Z > 0" (OFDM.c:858-866) except for an exactly-zero equalised value.
+template <int KIND>
+struct EqOut {
+    float2 u;
+    float r;    // unused for KIND 0
+};
+struct SymState {
+    float evm_pre;     // KIND 2: sum of (|Z - d| / 2)^2; scaled once per symbol by finish_evm
+    uint32_t be, ax;   // bit errors, slicer axis errors
+    uint32_t d[3];     // decided bits, DUMP only
+};
 
-template <bool DUMP, int R, typename HF>
+__device__ __forceinline__ void sym_init(SymState &st) {
+    st.evm_pre = 0.f; st.be = 0u; st.ax = 0u; st.d[0] = st.d[1] = st.d[2] = 0u;
+}
+template <int KIND>
+__device__ __forceinline__ float finish_evm(const SymState &st) { return KIND == 2 ? 4.0f * st.evm_pre : st.evm_pre; }
+
+template <bool DUMP, int R, int KIND, typename HF>
 __device__ __forceinline__ void demap_sub(const float2 (&x)[64], const uint32_t (&wi)[3], HF &&Hof, float2 *dump_eq,
                                           SymState &st) {
     uint32_t w[3] = {wi[0], wi[1], wi[2]};
-    opaque(w[0]); opaque(w[1]); opaque(w[2]);     // truth selects are made here, not hoisted
+    opaque(w[0]); opaque(w[1]); opaque(w[2]);     // truth shifts are made here, not hoisted
+    // b0 at bit 31 - 2m of w; b0 ^ b1 at the same position of wx
+    const uint32_t wx[3] = {w[0] ^ (w[0] << 1), w[1] ^ (w[1] << 1), w[2] ^ (w[2] << 1)};
+    constexpr float cd = KIND == 2 ? 0.5f * INV_SQRT2 : INV_SQRT2;
+    uint32_t em = 0u;     // per bin: re error then im error, shifted in from bit 0
     static_for<0, 16>([&](auto kc) {
         constexpr int bin = 4 * decltype(kc)::value + R;
         constexpr int m = data_index(bin);
         if constexpr (m >= 0) {
-            const float2 z = Hof(x[digit_rev4(bin)], std::integral_constant<int, bin>{});
-            if constexpr (DUMP) { if (dump_eq) dump_eq[m] = z; }
-            const uint32_t pr = z.x > 0.f, pi = z.y > 0.f;
-            constexpr int s0 = 31 - ((2 * m) & 31), s1 = 31 - ((2 * m + 1) & 31), wi = (2 * m) >> 5;
-            st.d[wi] |= ((pi ^ 1u) << s0) | ((pr ^ pi) << s1);
-            const uint32_t b0 = bit_of(w, 2 * m), b1 = bit_of(w, 2 * m + 1);
-            const float dr = (b0 == b1) ? INV_SQRT2 : -INV_SQRT2;
-            const float di = b0 ? -INV_SQRT2 : INV_SQRT2;
-            const float ex = z.x - dr, ey = z.y - di;
+            const EqOut<KIND> e = Hof(x[digit_rev4(bin)], std::integral_constant<int, bin>{});
+            constexpr int wi = (2 * m) >> 5, sh = (2 * m) & 31;
+            const uint32_t tr = sh ? wx[wi] << sh : wx[wi], ti = sh ? w[wi] << sh : w[wi];
+            // u' = u ^ (t & 0x80000000): bitop3 table a ^ (b & c) = 0x78
+            const uint32_t ur = __builtin_amdgcn_bitop3_b32(__float_as_uint(e.u.x), tr, 0x80000000u, 0x78);
+            const uint32_t ui = __builtin_amdgcn_bitop3_b32(__float_as_uint(e.u.y), ti, 0x80000000u, 0x78);
+            float ex, ey;
+            if constexpr (KIND == 0) {
+                ex = __uint_as_float(ur) - cd;
+                ey = __uint_as_float(ui) - cd;
+            } else {
+                ex = fmaf(__uint_as_float(ur), e.r, -cd);
+                ey = fmaf(__uint_as_float(ui), e.r, -cd);
+            }
             st.evm_pre = fmaf(ex, ex, fmaf(ey, ey, st.evm_pre));
+            em = __builtin_amdgcn_alignbit(em, ur, 31);
+            em = __builtin_amdgcn_alignbit(em, ui, 31);
+            if constexpr (DUMP) {
+                const float g = KIND == 0 ? 1.0f : KIND == 1 ? e.r : 2.0f * e.r;
+                const float2 z = KIND == 0 ? e.u : make_float2(e.u.x * g, e.u.y * g);
+                if (dump_eq) dump_eq[m] = z;
+                const uint32_t pr = z.x > 0.f, pi = z.y > 0.f;
+                constexpr int s0 = 31 - ((2 * m) & 31), s1 = 31 - ((2 * m + 1) & 31);
+                st.d[wi] |= ((pi ^ 1u) << s0) | ((pr ^ pi) << s1);
+            }
         }
     });
+    // im errors at even positions, re errors at odd: b0 wrong <=> im wrong, b1 wrong <=> re ^ im
+    st.ax += __popc(em);
+    st.be += __popc(em & 0x55555555u) + __popc((em ^ (em >> 1)) & 0x55555555u);
 }
 
-__device__ __forceinline__ void symbol_errors(const SymState &st, const uint32_t (&w)[3], uint32_t &be, uint32_t &ax) {
-    be = 0; ax = 0;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const uint32_t e = st.d[i] ^ w[i];
-        const uint32_t e0 = e & 0xAAAAAAAAu, e1 = e & 0x55555555u;   // b0 (imag axis) / b1 positions
-        be += __popc(e);
-        ax += __popc(e0) + __popc((e0 >> 1) ^ e1);                     // im wrong + (re xor im) wrong
-    }
+// dpp(a) + b as one v_add_f32_dpp (bound_ctrl lets the DPP combiner fold the move)
+template <int CTRL>
+__device__ __forceinline__ float dpp_add(float a, float b) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(a), CTRL, 0xF, 0xF, true)) + b;
+}
+
+// LTF least-squares equaliser for a quad {LTF1, LTF2, D0, D1} of one frame: S = F1 + F2 from
+// lanes 0 and 1, H = 0.5 Lf S (OFDM.c:846-849), Z = Y / H = 2 Lf Y conj(S) / |S|^2 (OFDM.c:1044-1052).
+template <int BIN>
+__device__ __forceinline__ EqOut<2> ls_equalise(float2 Y) {
+    const float2 F2 = dpp_c<DPP_QUAD_BCAST1>(Y);
+    const float2 S = make_float2(dpp_add<DPP_QUAD_BCAST0>(Y.x, F2.x), dpp_add<DPP_QUAD_BCAST0>(Y.y, F2.y));
+    EqOut<2> e;
+    e.r = __builtin_amdgcn_rcpf(fmaf(S.x, S.x, S.y * S.y));
+    e.u = cscale(cmulc(Y, S), (float)ltf_sign(BIN));
+    return e;
 }
 
 // frame-level counters of one wave, reduced and added into the block's LDS slots

@@ -213,28 +213,26 @@ __device__ __forceinline__ void rx_window_stage1(float2 (&x)[64], const WS &src,
 
 // Shared tail: FFT sub-blocks + demap, per-frame combine of the two data symbols (quad xor-1
 // partner), counters.  `leader` lanes (one per valid frame) contribute.
-template <bool DUMP, typename HF>
+template <bool DUMP, int KIND, typename HF>
 __device__ __forceinline__ void finish_symbol(float2 (&x)[64], const uint32_t (&w)[3], HF &&Hof, float2 *dump_eq,
                                               uint32_t *dump_bits, bool leader, unsigned long long *slots) {
     SymState st;
-    st.evm_pre = 0.f;
-    st.d[0] = st.d[1] = st.d[2] = 0u;
+    sym_init(st);
     static_for<0, 4>([&](auto rc) {
         constexpr int R = decltype(rc)::value;
         dif_sub16<false, R>(x);
-        demap_sub<DUMP, R>(x, w, Hof, dump_eq, st);
+        demap_sub<DUMP, R, KIND>(x, w, Hof, dump_eq, st);
         sched_fence();
     });
     if constexpr (DUMP) {
         if (dump_bits) { dump_bits[0] = st.d[0]; dump_bits[1] = st.d[1]; dump_bits[2] = st.d[2]; }
     }
-    uint32_t be, ax;
-    symbol_errors(st, w, be, ax);
-    const float e_other = dpp_f<DPP_QUAD_XOR1>(st.evm_pre);
-    const uint32_t be_other = dpp_u<DPP_QUAD_XOR1>(be);
-    const uint32_t ax_other = dpp_u<DPP_QUAD_XOR1>(ax);
+    const float evm = finish_evm<KIND>(st);
+    const float e_other = dpp_f<DPP_QUAD_XOR1>(evm);
+    const uint32_t be_other = dpp_u<DPP_QUAD_XOR1>(st.be);
+    const uint32_t ax_other = dpp_u<DPP_QUAD_XOR1>(st.ax);
     FrameAcc acc;
-    if (leader) frame_metrics(acc, st.evm_pre + e_other, be + be_other, ax + ax_other);
+    if (leader) frame_metrics(acc, evm + e_other, st.be + be_other, st.ax + ax_other);
     flush_wave(acc, slots);
 }
 
@@ -320,16 +318,8 @@ __global__ __launch_bounds__(256, OFDM_RX_WAVES_PER_SIMD) void rx_ls_kernel(RxAr
                 }
             }
             // H[k] = 0.5 (F1[k] + F2[k]) conj(Lf[k]), Lf = +-1 on data bins (OFDM.c:846-849)
-            auto Hof = [&](float2 Y, auto binc) {
-                constexpr int bin = decltype(binc)::value;
-                // with S = F1 + F2 and H = 0.5 Lf S (Lf = +-1): Y / H = Y conj(S) * (2 Lf / |S|^2)
-                constexpr float hs = 2.0f * (float)ltf_sign(bin);
-                const float2 F1 = dpp_c<DPP_QUAD_BCAST0>(Y), F2 = dpp_c<DPP_QUAD_BCAST1>(Y);
-                const float2 S = make_float2(F1.x + F2.x, F1.y + F2.y);
-                const float inv = hs * __builtin_amdgcn_rcpf(fmaf(S.x, S.x, S.y * S.y));
-                return cscale(cmulc(Y, S), inv);
-            };
-            finish_symbol<DUMP>(x, wq, Hof, dump_eq, dump_bits, role == 2 && valid, sacc[q]);
+            auto Hof = [&](float2 Y, auto binc) { return ls_equalise<decltype(binc)::value>(Y); };
+            finish_symbol<DUMP, 2>(x, wq, Hof, dump_eq, dump_bits, role == 2 && valid, sacc[q]);
         }
     }
     block_flush(a, sacc);
@@ -383,22 +373,24 @@ __global__ __launch_bounds__(256, OFDM_RX_WAVES_PER_SIMD) void rx_ideal_kernel(R
                 }
             }
             // perfect CSI: H[i] = c_i sum_l h_l e^{-j2pi(i-32)l/64}, c_i = (-1)^i for the C ifft (D5)
+            constexpr int KIND = CHAN == OFDM_CHAN_AWGN ? 0 : 1;
             auto Hof = [&](float2 Y, auto binc) {
                 constexpr int bin = decltype(binc)::value;
                 constexpr float cs = (CONV == OFDM_CONV_C && (bin & 1)) ? -1.0f : 1.0f;
+                EqOut<KIND> e;
                 if constexpr (CHAN == OFDM_CHAN_AWGN) {
-                    return cscale(Y, cs);
+                    e.u = cscale(Y, cs);
                 } else {
                     float2 H = hq[0];
                     H = csub(H, twiddle<bin * 1, false>(hq[1]));     // e^{-j2pi(i-32)l/64} = (-1)^l W^{il}
                     H = cadd(H, twiddle<bin * 2, false>(hq[2]));
                     H = csub(H, twiddle<bin * 3, false>(hq[3]));
-                    H = cscale(H, cs);
-                    const float inv = __builtin_amdgcn_rcpf(fmaf(H.x, H.x, H.y * H.y));
-                    return cscale(cmulc(Y, H), inv);
+                    e.r = __builtin_amdgcn_rcpf(fmaf(H.x, H.x, H.y * H.y));
+                    e.u = cscale(cmulc(Y, H), cs);                  // Y / (cs H) = cs Y conj(H) / |H|^2
                 }
+                return e;
             };
-            finish_symbol<DUMP>(x, wq, Hof, dump_eq, dump_bits, d == 0 && valid, sacc[q]);
+            finish_symbol<DUMP, KIND>(x, wq, Hof, dump_eq, dump_bits, d == 0 && valid, sacc[q]);
         }
     }
     block_flush(a, sacc);
