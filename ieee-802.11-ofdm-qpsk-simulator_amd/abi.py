@@ -6,6 +6,7 @@ missing or cannot be loaded, load_library() raises.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from pathlib import Path
 
 PKG_DIR = Path(__file__).resolve().parent
@@ -98,7 +99,8 @@ def load_library(path: Path | str | None = None) -> C.CDLL:
     global _LIB
     if _LIB is not None and path is None:
         return _LIB
-    p = Path(path or LIB_PATH)
+    # OFDM_MI355X_LIB: load a variant build (tools/build_variants.py) instead of the default
+    p = Path(path or os.environ.get("OFDM_MI355X_LIB") or LIB_PATH)
     try:
         # PyTorch ships its own libamdhip64 (same SONAME).  Loading it first makes this library
         # bind to that one HIP runtime instead of starting a second one from /opt/rocm, which

@@ -26,8 +26,8 @@ CFLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-fno-slp-vecto
           "-mllvm", "-amdgpu-atomic-optimizer-strategy=None", f"-I{INCLUDE}", f"-I{CSRC}"]
 
 
-def _compile(src: str, extra: list[str]) -> Path:
-    obj = BUILD / (Path(src).stem + ".o")
+def _compile(src: str, extra: list[str], build_dir: Path = BUILD) -> Path:
+    obj = build_dir / (Path(src).stem + ".o")
     cmd = [HIPCC, *CFLAGS, *extra, "-c", str(CSRC / src), "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
@@ -43,22 +43,26 @@ def _stale() -> bool:
     return any(p.stat().st_mtime > t for p in deps)
 
 
-def build(force: bool = False, extra: list[str] | None = None, verbose: bool = True) -> Path:
-    if not force and not _stale():
+def build(force: bool = False, extra: list[str] | None = None, verbose: bool = True,
+          out: Path | None = None) -> Path:
+    """Build the library (default: in-tree LIB).  `out` + `extra` make a variant build (own objects)."""
+    lib = Path(out) if out else LIB
+    if out is None and not force and not _stale():
         return LIB
-    BUILD.mkdir(exist_ok=True)
+    build_dir = BUILD if out is None else lib.parent / ("_build_" + lib.stem)
+    build_dir.mkdir(parents=True, exist_ok=True)
     extra = extra or []
     with ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
-        objs = list(ex.map(lambda s: _compile(s, extra), SOURCES))
-    tmp = LIB.with_suffix(".so.tmp")
+        objs = list(ex.map(lambda s: _compile(s, extra, build_dir), SOURCES))
+    tmp = lib.with_suffix(".so.tmp")
     cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
-    os.replace(tmp, LIB)
+    os.replace(tmp, lib)
     if verbose:
-        print(f"built {LIB}", file=sys.stderr)
-    return LIB
+        print(f"built {lib}", file=sys.stderr)
+    return lib
 
 
 if __name__ == "__main__":

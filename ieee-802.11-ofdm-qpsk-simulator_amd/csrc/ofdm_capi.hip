@@ -162,8 +162,17 @@ int ofdm_ctx_create(int device, ofdm_ctx **out) {
     for (int conv = 0; conv < 2; ++conv) {
         std::vector<float2> t;
         host_ltf_time(conv, t);
+        // 2T by staged row for the LS receiver: row r of a group holds window sample n = r - 4
+        // (rows start 3+1 samples into the CP for the 4-tap channel), cyclic in T
+        std::vector<float2> t2(68 * 2);
+        for (int r = 0; r < 68; ++r) {
+            const float2 v = t[(r - 4 + 64) & 63];
+            t2[2 * r] = t2[2 * r + 1] = make_float2(2.0f * v.x, 2.0f * v.y);
+        }
         if (hipMalloc(&c->d_ltf[conv], 64 * sizeof(float2)) != hipSuccess ||
-            hipMemcpy(c->d_ltf[conv], t.data(), 64 * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess) {
+            hipMemcpy(c->d_ltf[conv], t.data(), 64 * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess ||
+            hipMalloc(&c->d_ltf2_rows[conv], t2.size() * sizeof(float2)) != hipSuccess ||
+            hipMemcpy(c->d_ltf2_rows[conv], t2.data(), t2.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess) {
             ofdm_ctx_destroy(reinterpret_cast<ofdm_ctx *>(c));
             return set_error(OFDM_E_NOMEM, "LTF table upload failed");
         }
@@ -180,7 +189,7 @@ int ofdm_ctx_destroy(ofdm_ctx *ctx) {
     for (auto &e : c->done) { hipEventDestroy(e.a); hipEventDestroy(e.b); }
     for (auto &e : c->open) { hipEventDestroy(e.a); hipEventDestroy(e.b); }
     for (auto ev : c->pool) hipEventDestroy(ev);
-    for (void *p : {(void *)c->d_ltf[0], (void *)c->d_ltf[1], c->d_tx, c->d_bits, c->d_cnt, c->d_scratch,
+    for (void *p : {(void *)c->d_ltf[0], (void *)c->d_ltf[1], (void *)c->d_ltf2_rows[0], (void *)c->d_ltf2_rows[1], c->d_tx, c->d_bits, c->d_cnt, c->d_scratch,
                     c->d_scratch2, c->d_wave})
         if (p) hipFree(p);
     if (c->own) hipStreamDestroy(c->own);
@@ -243,10 +252,11 @@ int ofdm_fft64(ofdm_ctx *ctx, const void *d_in, void *d_out, int64_t n, int inve
 }
 
 int ofdm_tx_bytes(int64_t n_frames, int64_t *tx_bytes, int64_t *bits_bytes) {
-    if (n_frames < 0) return set_error(OFDM_E_ARG, "n_frames < 0");
-    const int64_t t = tiles_for(n_frames);
-    if (tx_bytes) *tx_bytes = t * SYM_SAMPLES * TILE_SYMBOLS * (int64_t)sizeof(float2);
-    if (bits_bytes) *bits_bytes = t * 3 * TILE_SYMBOLS * (int64_t)sizeof(uint32_t);
+    if (n_frames < 0 || n_frames > MAX_BATCH_FRAMES)
+        return set_error(OFDM_E_ARG, "n_frames %lld outside [0, %lld]", (long long)n_frames, (long long)MAX_BATCH_FRAMES);
+    const int64_t p = sym_pitch(n_frames);
+    if (tx_bytes) *tx_bytes = SYM_SAMPLES * p * (int64_t)sizeof(float2);
+    if (bits_bytes) *bits_bytes = 3 * p * (int64_t)sizeof(uint32_t);
     return OFDM_OK;
 }
 
@@ -257,13 +267,15 @@ int ofdm_tx_frames(ofdm_ctx *ctx, const ofdm_cfg *cfg, uint64_t first_frame, int
     int rc = check_cfg(cfg);
     if (rc) return rc;
     if (n_frames < 0 || (n_frames && (!d_tx || !d_bits))) return set_error(OFDM_E_ARG, "bad tx buffers");
+    if (n_frames > MAX_BATCH_FRAMES) return set_error(OFDM_E_ARG, "n_frames > %lld per batch", (long long)MAX_BATCH_FRAMES);
     if (n_frames == 0) return OFDM_OK;
     HIPOK(hipSetDevice(c->device));
     TxArgs a{};
     a.tx = (float2 *)d_tx;
     a.bits = (uint32_t *)d_bits;
     a.first_symbol = 2 * first_frame;
-    a.n_sym = tiles_for(n_frames) * TILE_SYMBOLS;
+    a.pitch = sym_pitch(n_frames);
+    a.n_sym = (2 * n_frames + 63) / 64 * 64;
     a.k0 = (uint32_t)cfg->seed;
     a.k1 = (uint32_t)(cfg->seed >> 32);
     a.payload = cfg->payload;
@@ -282,20 +294,21 @@ static int rx_common(Ctx *c, const ofdm_cfg *cfg, const void *d_tx, const void *
     if (rc) return rc;
     if (n_snr < 0 || (n_snr && !snr_db) || !d_counters) return set_error(OFDM_E_ARG, "bad snr/counters");
     if (n_frames < 0 || (n_frames && (!d_tx || !d_bits))) return set_error(OFDM_E_ARG, "bad rx buffers");
+    if (n_frames > MAX_BATCH_FRAMES) return set_error(OFDM_E_ARG, "n_frames > %lld per batch", (long long)MAX_BATCH_FRAMES);
     if (n_frames == 0 || n_snr == 0) return OFDM_OK;
     const bool dump = d_eq || d_dbits;
     if (dump && (!d_eq || !d_dbits)) return set_error(OFDM_E_ARG, "dump needs both d_eq and d_dbits");
     HIPOK(hipSetDevice(c->device));
-    const int64_t n_tiles = tiles_for(n_frames);
-    const unsigned grid = (unsigned)rx_grid(*cfg, n_tiles, c->device);
+    const unsigned grid = (unsigned)rx_grid(*cfg, n_frames, c->device);
     for (int q0 = 0; q0 < n_snr; q0 += OFDM_MAX_SNR) {
         RxArgs a{};
         a.tx = (const float2 *)d_tx;
         a.bits = (const uint32_t *)d_bits;
         a.ltf = c->d_ltf[cfg->conv];
+        a.ltf2_rows = c->d_ltf2_rows[cfg->conv];
         a.first_frame = first_frame;
         a.n_frames = n_frames;
-        a.n_tiles = n_tiles;
+        a.pitch = sym_pitch(n_frames);
         a.k0 = (uint32_t)cfg->seed;
         a.k1 = (uint32_t)(cfg->seed >> 32);
         a.n_snr = std::min(OFDM_MAX_SNR, n_snr - q0);
@@ -343,8 +356,8 @@ int ofdm_symbol_sweep(ofdm_ctx *ctx, const ofdm_cfg *cfg, const double *snr_db, 
     const size_t cbytes = (size_t)n_snr * OFDM_NCOUNTERS * sizeof(int64_t);
     if ((rc = c->ensure(&c->d_cnt, &c->cap_cnt, cbytes))) return rc;
     HIPOK(hipMemsetAsync(c->d_cnt, 0, cbytes, c->stream));
-    if (chunk_frames <= 0) chunk_frames = int64_t(1) << 22;           // 8.4M symbols, ~5.5 GB per chunk
-    chunk_frames = (chunk_frames + TILE_FRAMES - 1) / TILE_FRAMES * TILE_FRAMES;
+    if (chunk_frames <= 0) chunk_frames = int64_t(1) << 22;           // 8.4M symbols, ~5.4 GB per chunk
+    chunk_frames = std::min(chunk_frames, MAX_BATCH_FRAMES);
     const int64_t cf = std::min<int64_t>(chunk_frames, std::max<int64_t>(n_frames, 1));
     int64_t txb = 0, bb = 0;
     ofdm_tx_bytes(cf, &txb, &bb);

@@ -19,6 +19,7 @@ struct Ctx {
     hipStream_t own = nullptr;       // created by the context
     hipStream_t stream = nullptr;    // where work is enqueued (own or external)
     float2 *d_ltf[2] = {nullptr, nullptr};
+    float2 *d_ltf2_rows[2] = {nullptr, nullptr};   // LS staging column: [68][2] 2T[(r - 4) mod 64]
     // sweep scratch (grown on demand, freed with the context)
     void *d_tx = nullptr, *d_bits = nullptr, *d_cnt = nullptr, *d_scratch = nullptr, *d_scratch2 = nullptr;
     void *d_wave = nullptr;

@@ -9,21 +9,27 @@
 namespace ofdm {
 
 constexpr int OFDM_MAX_SNR = 64;       // SNR points per launch (the host splits larger grids)
-constexpr int TILE_SYMBOLS = 32;       // data symbols per Tx tile (16 frames x D = 2)
-constexpr int TILE_FRAMES = 16;
 constexpr int SYM_SAMPLES = 80;        // 64 + 16-sample cyclic prefix (OFDM.c:559-565)
 
-// tiles for n frames, rounded up to an even count so a 64-lane wave can always read 2 tiles
-inline int64_t tiles_for(int64_t n_frames) {
-    int64_t t = (n_frames + TILE_FRAMES - 1) / TILE_FRAMES;
-    return (t + 1) & ~int64_t(1);
-}
+// Tx batch layout, rows of symbols ("structure of arrays" over the batch):
+//   tx  [n * pitch + s] = time sample n (0..79, CP first) of data symbol s = 2 * frame + d
+//   bits[k * pitch + s] = payload word k (MSB-first bits 32k..32k+31) of symbol s
+// pitch = symbols rounded up to a whole wave plus one guard wave, so whole-wave reads and the LS
+// receiver's staged groups stay inside the buffer.
+inline int64_t sym_pitch(int64_t n_frames) { return (2 * n_frames + 63) / 64 * 64 + 64; }
+constexpr int64_t MAX_BATCH_FRAMES = int64_t(1) << 23;   // 80 * pitch fits int32 element offsets
+
+// LS receiver grouping: 21 frames per wave, lanes {E, D0, D1} x 21 + 1 idle
+constexpr int LS_GROUP_FRAMES = 21;
+constexpr int LS_GROUP_SYMS = 42;
+constexpr int LS_ROW_F2 = 44;          // staged LDS row: 42 data symbols + 2T sample (x2, one 16-B chunk)
 
 struct TxArgs {
     float2 *tx;
     uint32_t *bits;
     uint64_t first_symbol;
-    int64_t n_sym;                     // symbols to build (tiles * 32)
+    int64_t n_sym;                     // symbols to build (whole waves, < pitch)
+    int64_t pitch;
     uint32_t k0, k1;
     int32_t payload;
     uint32_t table[6];                 // MESSAGE / TESTER payload words (2 symbols x 3 words)
@@ -35,7 +41,8 @@ struct RxArgs {
     const float2 *ltf;                 // 64 time samples of one long training symbol (conv-specific)
     uint64_t first_frame;
     int64_t n_frames;
-    int64_t n_tiles;
+    int64_t pitch;
+    const float2 *ltf2_rows;           // LS: [row][2] 2T[(row + R0 - 16) mod 64], row pitch 16 B
     uint32_t k0, k1;
     int32_t n_snr;
     int32_t q_base;                    // global SNR index of sigma[0] (Philox stream id)
@@ -49,6 +56,6 @@ struct RxArgs {
 void launch_fft64(hipStream_t st, const float2 *in, float2 *out, int64_t n, int inverse, int conv);
 void launch_tx(hipStream_t st, const TxArgs &a, int conv);
 void launch_rx(hipStream_t st, const RxArgs &a, const ofdm_cfg &cfg, bool dump, unsigned grid);
-int rx_grid(const ofdm_cfg &cfg, int64_t n_tiles, int device);
+int rx_grid(const ofdm_cfg &cfg, int64_t n_frames, int device);
 
 }  // namespace ofdm

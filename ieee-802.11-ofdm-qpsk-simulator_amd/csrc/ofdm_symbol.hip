@@ -14,8 +14,11 @@
 #include "ofdm_internal.h"
 #include "ofdm_rxcommon.h"
 
-#ifndef OFDM_RX_WAVES_PER_SIMD
-#define OFDM_RX_WAVES_PER_SIMD 2
+#ifndef OFDM_RX_LS_WAVES            // waves per SIMD the LS receiver is register-budgeted for
+#define OFDM_RX_LS_WAVES 2
+#endif
+#ifndef OFDM_RX_IDEAL_WAVES
+#define OFDM_RX_IDEAL_WAVES 2
 #endif
 
 namespace ofdm {
@@ -112,41 +115,52 @@ __global__ __launch_bounds__(256, 3) void tx_symbols_kernel(TxArgs a) {
         static_for<0, 4>([&](auto ic) { dif_stage1<true, 4 * g + decltype(ic)::value>(X); });
         sched_fence();
     });
-    const int64_t tile = sidx >> 5;
-    const int slot = (int)(sidx & 31);
-    float2 *dst = a.tx + tile * (SYM_SAMPLES * TILE_SYMBOLS) + slot;
+    // row-major batch: sample n of symbol sidx at tx[n * pitch + sidx]; the row base
+    // is wave-uniform, so each store is saddr + one per-lane offset
+    const uint32_t so = (uint32_t)sidx;
+    const int64_t P = a.pitch;
     static_for<0, 4>([&](auto rc) {
         constexpr int R = decltype(rc)::value;
         dif_sub16<true, R>(X);
-        gf2 *d = (gf2 *)dst;
-        opaque(d);
         static_for<0, 16>([&](auto nc) {
             constexpr int n = 4 * decltype(nc)::value + R;                   // time samples n & 3 == R
             const float2 v = cscale(X[digit_rev4(n)], (n & 1) ? -1.0f / 64.0f : 1.0f / 64.0f);
-            gst(d, (16 + n) * TILE_SYMBOLS, v);
-            if constexpr (n >= 48) gst(d, (n - 48) * TILE_SYMBOLS, v);           // CP = last 16 samples
+            gst((gf2 *)(a.tx + (16 + n) * P), so, v);
+            if constexpr (n >= 48) gst((gf2 *)(a.tx + (n - 48) * P), so, v);   // CP = last 16 samples
         });
         sched_fence();
     });
-    uint32_t *bd = a.bits + tile * (3 * TILE_SYMBOLS) + slot;
-    bd[0] = w[0]; bd[TILE_SYMBOLS] = w[1]; bd[2 * TILE_SYMBOLS] = w[2];
+    a.bits[so] = w[0];
+    a.bits[P + so] = w[1];
+    a.bits[2 * P + so] = w[2];
 }
 
 // ======================================================================== K3: receiver chain
-// Clean sample n of a window: data windows read row 16+n of the Tx tile (n >= -3 reaches into the
-// CP), LTF windows read the cyclic training symbol T[(n + 64) & 63].
-// P is a global (gcf2) or LDS (lcf2) view.
-template <typename P>
-struct WindowSrc {
-    P *p;                // data: &tile[16][slot]; LTF: T
-    int stride;          // 32 (data) or 1 (LTF)
-    bool circ;           // LTF
+// Where the clean samples of a lane's window come from.  Both sources index sample n (-3..63,
+// negative = cyclic prefix, reached only by the 4-tap channel) with a compile-time offset.
+// GlobalRows: sample n of symbol s at row16[n * pitch + s] (row-major batch, wave-uniform row base,
+// so loads use saddr + one per-lane offset).
+struct GlobalRows {
+    const float2 *row16;
+    int64_t pitch;
+    uint32_t s;
+    __device__ __forceinline__ void fresh() {
+        // uniform operands too: otherwise all 64 row addresses are hoisted into SGPRs and spill
+        asm volatile("" : "+s"(row16), "+s"(pitch));
+        opaque(s);
+    }
+    template <int N>
+    __device__ __forceinline__ float2 at() const { return gld((gcf2 *)(row16 + N * pitch), (int)s); }
 };
-template <typename P>
-__device__ __forceinline__ float2 src_at(P *p, int stride, bool circ, int n) {
-    if (n >= 0) return ld2(p, n * stride);
-    return circ ? ld2(p, 64 + n) : ld2(p, n * stride);
-}
+// LdsRows: the LS receiver's staged group, LS_ROW_F2 float2 per row starting at sample R0 - 16;
+// base = this lane's column (a data symbol, or the 2T column for the LTF-pair lane).
+template <int R0>
+struct LdsRows {
+    lcf2 *base;
+    __device__ __forceinline__ void fresh() { opaque(base); }
+    template <int N>
+    __device__ __forceinline__ float2 at() const { return ld2(base, (N + 16 - R0) * LS_ROW_F2); }
+};
 
 // Load + channel + AWGN for samples n0..n0+3, times (-1)^n (fft() = DFT of x(-1)^n, OFDM.c:314-318).
 // Noise sample at frame time t uses Gaussian t (real) or 2t, 2t+1 (complex) of the frame's stream
@@ -156,9 +170,10 @@ __device__ __forceinline__ void rx_block(float2 (&x)[64], const WS &src, uint32_
                                          uint32_t t0, uint32_t q, float sigma, uint32_t k0, uint32_t k1,
                                          const float2 (&h)[4]) {
     // re-materialise per block: keeps LICM from hoisting 16 blocks' worth of addresses / round-1 products
-    auto p = src.p;
+    WS p = src;
+    p.fresh();
     uint32_t flo = f_lo, fhi = f_hi, tb = t0;
-    opaque(p); opaque(flo); opaque(fhi); opaque(tb);
+    opaque(flo); opaque(fhi); opaque(tb);
     f_lo = flo; f_hi = fhi; t0 = tb;
     float z[8];
     if constexpr (NOISE == OFDM_NOISE_REAL) {
@@ -172,9 +187,9 @@ __device__ __forceinline__ void rx_block(float2 (&x)[64], const WS &src, uint32_
     }
     float2 c[7];
     if constexpr (CHAN == OFDM_CHAN_RAYLEIGH4) {
-        static_for<0, 7>([&](auto ic) { c[decltype(ic)::value] = src_at(p, src.stride, src.circ, N0 - 3 + decltype(ic)::value); });
+        static_for<0, 7>([&](auto ic) { c[decltype(ic)::value] = p.template at<N0 - 3 + decltype(ic)::value>(); });
     } else {
-        static_for<0, 4>([&](auto ic) { c[3 + decltype(ic)::value] = src_at(p, src.stride, src.circ, N0 + decltype(ic)::value); });
+        static_for<0, 4>([&](auto ic) { c[3 + decltype(ic)::value] = p.template at<N0 + decltype(ic)::value>(); });
     }
     static_for<0, 4>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
@@ -211,11 +226,13 @@ __device__ __forceinline__ void rx_window_stage1(float2 (&x)[64], const WS &src,
     });
 }
 
-// Shared tail: FFT sub-blocks + demap, per-frame combine of the two data symbols (quad xor-1
-// partner), counters.  `leader` lanes (one per valid frame) contribute.
-template <bool DUMP, int KIND, typename HF>
-__device__ __forceinline__ void finish_symbol(float2 (&x)[64], const uint32_t (&w)[3], HF &&Hof, float2 *dump_eq,
-                                              uint32_t *dump_bits, bool leader, unsigned long long *slots) {
+// Shared tail: FFT sub-blocks + demap, per-frame combine of the frame's two data symbols
+// (`partner` fetches the other data lane's value), counters.  `leader` lanes (one per valid
+// frame) contribute.
+template <bool DUMP, int KIND, typename HF, typename PF>
+__device__ __forceinline__ void finish_symbol(float2 (&x)[64], const uint32_t (&w)[3], HF &&Hof, PF &&partner,
+                                              float2 *dump_eq, uint32_t *dump_bits, bool leader,
+                                              unsigned long long *slots) {
     SymState st;
     sym_init(st);
     static_for<0, 4>([&](auto rc) {
@@ -228,106 +245,137 @@ __device__ __forceinline__ void finish_symbol(float2 (&x)[64], const uint32_t (&
         if (dump_bits) { dump_bits[0] = st.d[0]; dump_bits[1] = st.d[1]; dump_bits[2] = st.d[2]; }
     }
     const float evm = finish_evm<KIND>(st);
-    const float e_other = dpp_f<DPP_QUAD_XOR1>(evm);
-    const uint32_t be_other = dpp_u<DPP_QUAD_XOR1>(st.be);
-    const uint32_t ax_other = dpp_u<DPP_QUAD_XOR1>(st.ax);
+    const float e_other = __uint_as_float(partner(__float_as_uint(evm)));
+    const uint32_t be_other = partner(st.be), ax_other = partner(st.ax);
     FrameAcc acc;
     if (leader) frame_metrics(acc, evm + e_other, st.be + be_other, st.ax + ax_other);
     flush_wave(acc, slots);
 }
 
-// ---- LS estimate: quad = {LTF1, LTF2, D0, D1} of one frame; wave = 16 frames = one tile ----
-// Each wave stages the rows of its tile the windows read (16..79, or 12..79 when the 4-tap channel
-// reaches 3 samples into the CP) into its own LDS slice once, with global_load_lds_dwordx4 (1 KB per
-// wave instruction), so the n_snr passes over the tile read LDS instead of re-fetching HBM/L2.
+// ---- LS estimate: a wave carries 21 frames, lanes {E, D0, D1} per frame (lane 63 idle) ----
+// H = 0.5 (F1 + F2) conj(Lf) (OFDM.c:830-850) with F1 + F2 = FFT(r1 + r2) (linearity).  Both LTF
+// windows hold the same clean samples T, so the E lane transforms 2T (+ channel) plus the pair's
+// noise n1 + n2, drawn once as sqrt(2) sigma x the LTF1-slot Gaussians (same law).
+// The data lanes fetch S = F1 + F2 from their E lane with ds_bpermute.
+//
+// The 4 waves of a block share one staged group (42 symbols x 64-68 rows, plus the 2T column)
+// in LDS and split the SNR points; the next group is prefetched by LDS-DMA into the other buffer.
 template <int CHAN>
-struct LsStage {
-    static constexpr int R0 = CHAN == OFDM_CHAN_RAYLEIGH4 ? 12 : 16;
+struct LsGroup {
+    static constexpr int R0 = CHAN == OFDM_CHAN_RAYLEIGH4 ? 12 : 16;   // first staged sample row
     static constexpr int ROWS = SYM_SAMPLES - R0;
-    static constexpr int BYTES = ROWS * TILE_SYMBOLS * 8;
-    static constexpr int CHUNKS = BYTES / 1024;
-    static_assert(BYTES % 1024 == 0, "staged rows must be whole 1 KB wave chunks");
+    static constexpr int ROW_CHUNKS = LS_ROW_F2 / 2;                  // 16-B chunks per staged row
+    static constexpr int CHUNKS = ROWS * ROW_CHUNKS;
+    static constexpr int BUF_F2 = ROWS * LS_ROW_F2;
+    static_assert(LS_GROUP_SYMS / 2 + 1 == ROW_CHUNKS, "42 data symbols + one 2T chunk per row");
 };
 
+template <int CHAN>
+__device__ __forceinline__ void ls_stage(const RxArgs &a, int64_t grp, float2 *buf, int wv, int lane) {
+    using G = LsGroup<CHAN>;
+    const float2 *col0 = a.tx + grp * LS_GROUP_SYMS;
+    for (int k = wv; k * 64 < G::CHUNKS; k += 4) {
+        const int c = k * 64 + lane;                    // chunk c lands at LDS byte 16 c (M0 + 16 lane)
+        if (c < G::CHUNKS) {
+            const int row = c / G::ROW_CHUNKS, j = c - row * G::ROW_CHUNKS;
+            const char *src = j < LS_GROUP_SYMS / 2
+                ? (const char *)(col0 + (int64_t)(G::R0 + row) * a.pitch) + j * 16
+                : (const char *)(a.ltf2_rows + 2 * (row + G::R0 - 12));
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)src,
+                                             (__attribute__((address_space(3))) void *)((char *)buf + k * 1024),
+                                             16, 0, 0);
+        }
+    }
+}
+
+template <int BIN>
+__device__ __forceinline__ EqOut<2> ls_equalise_bp(float2 Y, uint32_t e_addr) {
+    // S[k] = F1[k] + F2[k] from the frame's E lane; Z = Y / (0.5 Lf S) = 2 Lf Y conj(S) / |S|^2
+    const float2 S = make_float2(__int_as_float(__builtin_amdgcn_ds_bpermute((int)e_addr, __float_as_int(Y.x))),
+                                 __int_as_float(__builtin_amdgcn_ds_bpermute((int)e_addr, __float_as_int(Y.y))));
+    EqOut<2> e;
+    e.r = __builtin_amdgcn_rcpf(fmaf(S.x, S.x, S.y * S.y));
+    e.u = cscale(cmulc(Y, S), (float)ltf_sign(BIN));
+    return e;
+}
+
 template <int NOISE, int CHAN, bool DUMP>
-__global__ __launch_bounds__(256, OFDM_RX_WAVES_PER_SIMD) void rx_ls_kernel(RxArgs a) {
-    using St = LsStage<CHAN>;
+__global__ __launch_bounds__(256, OFDM_RX_LS_WAVES) void rx_ls_kernel(RxArgs a) {
+    using G = LsGroup<CHAN>;
     __shared__ unsigned long long sacc[OFDM_MAX_SNR][8];
-    __shared__ __attribute__((aligned(16))) float2 s_tile[4][St::ROWS * TILE_SYMBOLS];
-    __shared__ float2 s_ltf[64];
+    __shared__ __attribute__((aligned(16))) float2 sbuf[2][G::BUF_F2];
     for (int i = threadIdx.x; i < a.n_snr * 8; i += blockDim.x) (&sacc[0][0])[i] = 0ull;
-    if (threadIdx.x < 64) s_ltf[threadIdx.x] = a.ltf[threadIdx.x];
-    __syncthreads();
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
-    const int role = lane & 3, fi = lane >> 2;
-    const int64_t wave_id = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
-    const int64_t n_waves = (int64_t)gridDim.x * (blockDim.x >> 6);
-    // window start on the frame timeline: LTF1 192, LTF2 256, D0 336, D1 416
-    const uint32_t t0 = role == 0 ? 192u : role == 1 ? 256u : (role == 2 ? 336u : 416u);
-    const bool is_data = role >= 2;
-    const int slot = 2 * fi + (role & 1);
-    float2 *my_tile = s_tile[wv];
+    const int fr = lane / 3, role = lane - 3 * fr;     // lane 63: fr 21 (no frame), role 0
+    const bool is_e = role == 0;
+    const int col = is_e ? LS_GROUP_SYMS : 2 * fr + role - 1;
+    // window start on the frame timeline: LTF pair at the LTF1 slots 192, D0 336, D1 416
+    const uint32_t t0 = is_e ? 192u : 256u + 80u * (uint32_t)role;
+    const uint32_t e_addr = (uint32_t)(3 * fr) << 2;
+    const uint32_t d1_addr = (uint32_t)(lane + 1) << 2;
+    const int64_t n_groups = (a.n_frames + LS_GROUP_FRAMES - 1) / LS_GROUP_FRAMES;
+    const int64_t P = a.pitch;
 
-    for (int64_t tile = wave_id; tile < a.n_tiles; tile += n_waves) {
-        const int64_t fl = tile * TILE_FRAMES + fi;
-        const bool valid = fl < a.n_frames;
+    int cur = 0;
+    int64_t grp = blockIdx.x;
+    if (grp < n_groups) ls_stage<CHAN>(a, grp, sbuf[0], wv, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (; grp < n_groups; grp += gridDim.x) {
+        const int64_t fl = grp * LS_GROUP_FRAMES + fr;
+        const bool valid = fr < LS_GROUP_FRAMES && fl < a.n_frames;
         const uint64_t f = a.first_frame + (uint64_t)fl;
         const uint32_t f_lo = (uint32_t)f, f_hi = (uint32_t)(f >> 32);
-        {
-            // previous tile's LDS reads were consumed by its FFTs, so the slice is free to overwrite
-            const char *g = (const char *)(a.tx + tile * (SYM_SAMPLES * TILE_SYMBOLS) + St::R0 * TILE_SYMBOLS) + lane * 16;
-            static_for<0, St::CHUNKS>([&](auto cc) {
-                constexpr int c = decltype(cc)::value;
-                __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(g + c * 1024),
-                                                 (__attribute__((address_space(3))) void *)((char *)my_tile + c * 1024),
-                                                 16, 0, 0);
-            });
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        WindowSrc<lcf2> src;
-        src.p = is_data ? (lcf2 *)(my_tile + (16 - St::R0) * TILE_SYMBOLS + slot) : (lcf2 *)s_ltf;
-        src.stride = is_data ? TILE_SYMBOLS : 1;
-        src.circ = !is_data;
         uint32_t w[3] = {0u, 0u, 0u};
-        if (is_data) {
-            const uint32_t *bp = a.bits + tile * (3 * TILE_SYMBOLS) + slot;
-            w[0] = bp[0]; w[1] = bp[TILE_SYMBOLS]; w[2] = bp[2 * TILE_SYMBOLS];
+        if (!is_e && valid) {
+            const uint32_t so = (uint32_t)(grp * LS_GROUP_SYMS + col);
+            w[0] = a.bits[so]; w[1] = a.bits[P + so]; w[2] = a.bits[2 * P + so];
         }
+        // land the truth words before the prefetch is queued (vmcnt retires in issue order)
+        opaque(w[0]); opaque(w[1]); opaque(w[2]);
         float2 h[4] = {make_float2(1.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f)};
         if constexpr (CHAN == OFDM_CHAN_RAYLEIGH4) channel_taps(f_lo, f_hi, a.k0, a.k1, h);
+        const int64_t nxt = grp + gridDim.x;
+        if (nxt < n_groups) ls_stage<CHAN>(a, nxt, sbuf[cur ^ 1], wv, lane);
+        LdsRows<G::R0> src;
+        src.base = (lcf2 *)(sbuf[cur] + col);
 
-        for (int q = 0; q < a.n_snr; ++q) {
-            WindowSrc<lcf2> s = src;
+        for (int q = wv; q < a.n_snr; q += 4) {
+            LdsRows<G::R0> s = src;
             uint32_t wq[3] = {w[0], w[1], w[2]};
             uint32_t flo = f_lo, fhi = f_hi;
             float2 hq[4] = {h[0], h[1], h[2], h[3]};
-            opaque(s.p); opaque(wq[0]); opaque(wq[1]); opaque(wq[2]); opaque(flo); opaque(fhi);
+            s.fresh(); opaque(wq[0]); opaque(wq[1]); opaque(wq[2]); opaque(flo); opaque(fhi);
             if constexpr (CHAN == OFDM_CHAN_RAYLEIGH4) {
                 static_for<0, 4>([&](auto lc) { opaque(hq[decltype(lc)::value].x); opaque(hq[decltype(lc)::value].y); });
             }
+            const float sg = is_e ? a.sigma[q] * 1.41421356237309504880f : a.sigma[q];
             float2 x[64];
-            rx_window_stage1<NOISE, CHAN>(x, s, flo, fhi, t0, (uint32_t)(a.q_base + q), a.sigma[q], a.k0, a.k1, hq);
+            rx_window_stage1<NOISE, CHAN>(x, s, flo, fhi, t0, (uint32_t)(a.q_base + q), sg, a.k0, a.k1, hq);
             float2 *dump_eq = nullptr;
             uint32_t *dump_bits = nullptr;
             if constexpr (DUMP) {
-                if (is_data && valid) {
-                    const int64_t r = ((int64_t)q * a.dump_frames + fl) * 2 + (role & 1);
+                if (!is_e && valid) {
+                    const int64_t r = ((int64_t)q * a.dump_frames + fl) * 2 + (role - 1);
                     dump_eq = a.dump_eq + r * 48;
                     dump_bits = a.dump_bits + r * 3;
                 }
             }
-            // H[k] = 0.5 (F1[k] + F2[k]) conj(Lf[k]), Lf = +-1 on data bins (OFDM.c:846-849)
-            auto Hof = [&](float2 Y, auto binc) { return ls_equalise<decltype(binc)::value>(Y); };
-            finish_symbol<DUMP, 2>(x, wq, Hof, dump_eq, dump_bits, role == 2 && valid, sacc[q]);
+            auto Hof = [&](float2 Y, auto binc) { return ls_equalise_bp<decltype(binc)::value>(Y, e_addr); };
+            auto partner = [&](uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_bpermute((int)d1_addr, (int)v); };
+            finish_symbol<DUMP, 2>(x, wq, Hof, partner, dump_eq, dump_bits, role == 1 && valid, sacc[q]);
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // next group landed
+        __syncthreads();                                   // and every wave is done with this one
+        cur ^= 1;
     }
     block_flush(a, sacc);
 }
 
-// ---- ideal channel knowledge: every lane a data symbol; wave = 2 tiles = 32 frames ----
+// ---- ideal channel knowledge: every lane a data symbol; wave = 64 consecutive symbols ----
 template <int CONV, int NOISE, int CHAN, bool DUMP>
-__global__ __launch_bounds__(256, OFDM_RX_WAVES_PER_SIMD) void rx_ideal_kernel(RxArgs a) {
+__global__ __launch_bounds__(256, OFDM_RX_IDEAL_WAVES) void rx_ideal_kernel(RxArgs a) {
     __shared__ unsigned long long sacc[OFDM_MAX_SNR][8];
     for (int i = threadIdx.x; i < a.n_snr * 8; i += blockDim.x) (&sacc[0][0])[i] = 0ull;
     __syncthreads();
@@ -336,28 +384,27 @@ __global__ __launch_bounds__(256, OFDM_RX_WAVES_PER_SIMD) void rx_ideal_kernel(R
     const int64_t n_waves = (int64_t)gridDim.x * (blockDim.x >> 6);
     const int d = lane & 1;
     const uint32_t t0 = 336u + 80u * (uint32_t)d;
-    const int64_t n_pairs = (a.n_tiles + 1) >> 1;
-    for (int64_t pr = wave_id; pr < n_pairs; pr += n_waves) {
-        const int64_t tile = 2 * pr + (lane >> 5);
-        const int slot = lane & 31;
-        const int64_t fl = tile * TILE_FRAMES + (slot >> 1);
+    const int64_t n_sym = 2 * a.n_frames;
+    const int64_t P = a.pitch;
+    for (int64_t wg = wave_id; wg * 64 < n_sym; wg += n_waves) {
+        const uint32_t so = (uint32_t)(wg * 64 + lane);
+        const int64_t fl = (int64_t)(so >> 1);
         const bool valid = fl < a.n_frames;
         const uint64_t f = a.first_frame + (uint64_t)fl;
         const uint32_t f_lo = (uint32_t)f, f_hi = (uint32_t)(f >> 32);
-        WindowSrc<gcf2> src;
-        src.p = (gcf2 *)(a.tx + tile * (SYM_SAMPLES * TILE_SYMBOLS) + 16 * TILE_SYMBOLS + slot);
-        src.stride = TILE_SYMBOLS;
-        src.circ = false;
-        const uint32_t *bp = a.bits + tile * (3 * TILE_SYMBOLS) + slot;
-        uint32_t w[3] = {bp[0], bp[TILE_SYMBOLS], bp[2 * TILE_SYMBOLS]};
+        GlobalRows src;
+        src.row16 = a.tx + 16 * P;
+        src.pitch = P;
+        src.s = so;
+        uint32_t w[3] = {a.bits[so], a.bits[P + so], a.bits[2 * P + so]};
         float2 h[4] = {make_float2(1.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f)};
         if constexpr (CHAN == OFDM_CHAN_RAYLEIGH4) channel_taps(f_lo, f_hi, a.k0, a.k1, h);
         for (int q = 0; q < a.n_snr; ++q) {
-            WindowSrc<gcf2> s = src;
+            GlobalRows s = src;
             uint32_t wq[3] = {w[0], w[1], w[2]};
             uint32_t flo = f_lo, fhi = f_hi;
             float2 hq[4] = {h[0], h[1], h[2], h[3]};
-            opaque(s.p); opaque(wq[0]); opaque(wq[1]); opaque(wq[2]); opaque(flo); opaque(fhi);
+            s.fresh(); opaque(wq[0]); opaque(wq[1]); opaque(wq[2]); opaque(flo); opaque(fhi);
             if constexpr (CHAN == OFDM_CHAN_RAYLEIGH4) {
                 static_for<0, 4>([&](auto lc) { opaque(hq[decltype(lc)::value].x); opaque(hq[decltype(lc)::value].y); });
             }
@@ -372,7 +419,6 @@ __global__ __launch_bounds__(256, OFDM_RX_WAVES_PER_SIMD) void rx_ideal_kernel(R
                     dump_bits = a.dump_bits + r * 3;
                 }
             }
-            // perfect CSI: H[i] = c_i sum_l h_l e^{-j2pi(i-32)l/64}, c_i = (-1)^i for the C ifft (D5)
             constexpr int KIND = CHAN == OFDM_CHAN_AWGN ? 0 : 1;
             auto Hof = [&](float2 Y, auto binc) {
                 constexpr int bin = decltype(binc)::value;
@@ -390,7 +436,8 @@ __global__ __launch_bounds__(256, OFDM_RX_WAVES_PER_SIMD) void rx_ideal_kernel(R
                 }
                 return e;
             };
-            finish_symbol<DUMP, KIND>(x, wq, Hof, dump_eq, dump_bits, d == 0 && valid, sacc[q]);
+            auto partner = [](uint32_t v) { return dpp_u<DPP_QUAD_XOR1>(v); };
+            finish_symbol<DUMP, KIND>(x, wq, Hof, partner, dump_eq, dump_bits, d == 0 && valid, sacc[q]);
         }
     }
     block_flush(a, sacc);
@@ -448,15 +495,17 @@ void launch_rx(hipStream_t st, const RxArgs &a, const ofdm_cfg &cfg, bool dump, 
     }
 }
 
-int rx_grid(const ofdm_cfg &cfg, int64_t n_tiles, int device) {
-    // waves needed: one per tile (LS) or per tile pair (ideal); 4 waves per block
-    const int64_t waves = cfg.est == OFDM_EST_LS ? n_tiles : (n_tiles + 1) / 2;
-    const int64_t need = (waves + 3) / 4;
+int rx_grid(const ofdm_cfg &cfg, int64_t n_frames, int device) {
+    // LS: one block per 21-frame group in flight; ideal: one wave per 64 symbols, 4 waves per block
+    const int64_t need = cfg.est == OFDM_EST_LS ? (n_frames + LS_GROUP_FRAMES - 1) / LS_GROUP_FRAMES
+                                                : ((2 * n_frames + 63) / 64 + 3) / 4;
     int per_cu = 0, cus = 0;
     const void *k = cfg.est == OFDM_EST_LS
-        ? reinterpret_cast<const void *>(&rx_ls_kernel<OFDM_NOISE_REAL, OFDM_CHAN_AWGN, false>)
+        ? (cfg.channel == OFDM_CHAN_AWGN
+               ? reinterpret_cast<const void *>(&rx_ls_kernel<OFDM_NOISE_REAL, OFDM_CHAN_AWGN, false>)
+               : reinterpret_cast<const void *>(&rx_ls_kernel<OFDM_NOISE_REAL, OFDM_CHAN_RAYLEIGH4, false>))
         : reinterpret_cast<const void *>(&rx_ideal_kernel<OFDM_CONV_C, OFDM_NOISE_REAL, OFDM_CHAN_AWGN, false>);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, 0) != hipSuccess || per_cu < 1) per_cu = 2;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1) cus = 256;
     const int64_t cap = (int64_t)per_cu * cus;
     const int64_t g = need < cap ? need : cap;

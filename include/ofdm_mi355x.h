@@ -109,9 +109,10 @@ int ofdm_fft64(ofdm_ctx *ctx, const void *d_in, void *d_out, int64_t n, int inve
 
 /* ---- symbol-mode Monte Carlo (the per-symbol chain) ----
  * Tx batch ("Transmitter()", OFDM.c:467-618, for data symbols): frames [first_frame,
- * first_frame + n_frames) with D = 2 data symbols each.  Layout: tiles of 32 data
- * symbols; d_tx  = [tile][80 samples incl. CP][32] float2, d_bits = [tile][3 words][32] uint32
- * (MSB-first bits).  Buffer sizes: ofdm_tx_bytes(n_frames, &tx_bytes, &bits_bytes). */
+ * first_frame + n_frames) with D = 2 data symbols each (symbol s = 2 * frame + d).  Row-major
+ * layout: d_tx[n * pitch + s] = sample n (0..79, CP first) as float2, d_bits[k * pitch
+ * + s] = payload word k (MSB-first bits) as uint32, pitch = tx_bytes / (80 * 8).  Buffer sizes:
+ * ofdm_tx_bytes(n_frames, &tx_bytes, &bits_bytes); at most 2^23 frames per batch. */
 int ofdm_tx_bytes(int64_t n_frames, int64_t *tx_bytes, int64_t *bits_bytes);
 int ofdm_tx_frames(ofdm_ctx *ctx, const ofdm_cfg *cfg, uint64_t first_frame, int64_t n_frames,
                    void *d_tx, void *d_bits);

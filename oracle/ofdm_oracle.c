@@ -474,11 +474,24 @@ void orc_symbol_sweep(const orc_cfg *cfg, const double *snr_db, int n_snr,
 
             cplx H[NFFT];
             if (cfg->est == ORC_EST_LS) {
-                cplx r1[NFFT], r2[NFFT], F1[NFFT], F2[NFFT];
-                for (int n = 0; n < NFFT; ++n) RX_AT(192 + n, r1[n]);
-                for (int n = 0; n < NFFT; ++n) RX_AT(256 + n, r2[n]);
-                fft64c(r1, F1); fft64c(r2, F2);
-                for (int k = 0; k < NFFT; ++k) H[k] = 0.5 * (F1[k] + F2[k]) * conj(Lf[k]);
+                /* H = 0.5 (F1 + F2) conj(Lf) (OFDM.c:830-850) = 0.5 FFT(r1 + r2) conj(Lf).  The LTF
+                 * windows [192,256) and [256,320) carry the same clean samples (cyclic T, the channel
+                 * reaches back into T's tail either way), so r1 + r2 = 2 clean(192 + n) + (n1 + n2);
+                 * symbol mode draws the pair noise n1 + n2 once: sqrt(2) x the LTF1-slot Gaussians
+                 * (identical law). */
+                cplx e[NFFT], E[NFFT];
+                for (int n = 0; n < NFFT; ++n) {
+                    const int t = 192 + n;
+                    cplx acc = 0;
+                    for (int l = 0; l < 4; ++l) acc += h[l] * x[t - l];
+                    acc *= 2.0;
+                    if (cfg->noise == ORC_NOISE_REAL) acc += M_SQRT2 * sigma * gauss_at(&gc, f, q, (uint32_t)t);
+                    else if (cfg->noise == ORC_NOISE_COMPLEX)
+                        acc += sigma * (gauss_at(&gc, f, q, 2u * t) + I * gauss_at(&gc, f, q, 2u * t + 1));
+                    e[n] = acc;
+                }
+                fft64c(e, E);
+                for (int k = 0; k < NFFT; ++k) H[k] = 0.5 * E[k] * conj(Lf[k]);
             } else {
                 /* perfect channel knowledge: H[i] = c_i sum_l h_l e^{-j2pi(i-32)l/64},
                  * c_i = (-1)^i for the C ifft convention (D5), 1 for MATLAB */

@@ -62,18 +62,17 @@ def test_fft64_empty(engine):
 
 # ------------------------------------------------------------------ K2
 def tile_symbol(tx, bits, s):
-    """symbol s of the tiled Tx batch -> (80 samples, 3 words)"""
-    t, slot = divmod(s, 32)
-    txr = tx.view(-1, 80, 32)
-    br = bits.view(-1, 3, 32)
-    return txr[t, :, slot].cpu().numpy(), br[t, :, slot].cpu().numpy().astype(np.uint32)
+    """symbol s of the row-major Tx batch (tx[n * pitch + s], bits[k * pitch + s]) -> (80 samples, 3 words)"""
+    pitch = tx.numel() // 80
+    return (tx.view(80, pitch)[:, s].cpu().numpy(),
+            bits.view(3, pitch)[:, s].cpu().numpy().astype(np.uint32))
 
 
 @pytest.mark.parametrize("conv", ["c", "matlab"])
 @pytest.mark.parametrize("payload", ["random", "message", "tester"])
 def test_tx_symbols_vs_oracle(engine, oracle, pkg, conv, payload):
     cfg = pkg.make_cfg(conv=conv, payload=payload)
-    nf = 37  # ragged: not a multiple of the 16-frame tile
+    nf = 37  # ragged: not a multiple of a wave (32 frames) or an LS group (21 frames)
     tx, bits = engine.tx_frames(cfg, 1000, nf)
     for s in (0, 1, 17, 2 * nf - 1):
         samp, words = tile_symbol(tx, bits, s)

@@ -56,8 +56,10 @@ def test_tx_bytes(pkg):
     lib = pkg.load_library()
     tb, bb = C.c_int64(), C.c_int64()
     assert lib.ofdm_tx_bytes(17, C.byref(tb), C.byref(bb)) == 0
-    # 17 frames -> 2 tiles of 16 frames (rounded to an even count) x 32 symbols x 80 samples x 8 B
-    assert tb.value == 2 * 32 * 80 * 8 and bb.value == 2 * 3 * 32 * 4
+    # 17 frames = 34 symbols -> pitch = 64 (whole wave) + 64 (guard wave); rows of 80 samples x 8 B
+    assert tb.value == 80 * 128 * 8 and bb.value == 3 * 128 * 4
+    assert lib.ofdm_tx_bytes(1 << 23, C.byref(tb), C.byref(bb)) == 0
+    assert lib.ofdm_tx_bytes((1 << 23) + 1, C.byref(tb), C.byref(bb)) == -1     # int32 element offsets
 
 
 def test_write_float_array_format(pkg, tmp_path):
