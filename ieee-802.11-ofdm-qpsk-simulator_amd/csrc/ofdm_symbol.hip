@@ -15,10 +15,10 @@
 #include "ofdm_rxcommon.h"
 
 #ifndef OFDM_RX_LS_WAVES            // waves per SIMD the LS receiver is register-budgeted for
-#define OFDM_RX_LS_WAVES 2
+#define OFDM_RX_LS_WAVES 3
 #endif
 #ifndef OFDM_RX_IDEAL_WAVES
-#define OFDM_RX_IDEAL_WAVES 2
+#define OFDM_RX_IDEAL_WAVES 3
 #endif
 
 namespace ofdm {
