@@ -30,7 +30,6 @@ import ofdm_pkg  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BYTES_PER_SYMBOL_SNR = 652     # 80 x 8 B clean symbol + 12 B packed truth bits
-BYTES_LOADED_PER_SYMBOL_SNR = 524  # what K3 logically reads: the 64-sample FFT window + 12 B bits
 
 WORKLOADS = {
     # name: (config description, cfg kwargs, symbols per SNR point per GPU, snr grid)
@@ -45,16 +44,17 @@ WORKLOADS = {
 SNR_GRID = np.arange(0.0, 31.0, 2.0)
 
 
-def load_pmc_traffic(workload: str):
-    """HBM bytes per K3 launch from the committed rocprofv3 --pmc summary (profiles/), or None."""
+VALU_PEAK_PER_S = 256 * 4 * 0.5 * 2.4e9   # wave64 VALU instructions/s: 1 per 2 cycles per SIMD (tools/ubench_valu.hip)
+
+
+def load_pmc(workload: str) -> dict:
+    """Per-launch rocprofv3 --pmc figures for this workload (profiles/pmc_summary.json, written by
+    tools/pmc_summary.py from tools/gpu_profile.sh runs), or {}."""
     p = ROOT / "profiles" / "pmc_summary.json"
-    if not p.exists():
-        return None
     try:
-        d = json.loads(p.read_text())
-        return d.get(workload, {}).get("rx_hbm_bytes_per_launch")
+        return json.loads(p.read_text()).get(workload, {})
     except Exception:
-        return None
+        return {}
 
 
 def cpu_baseline(seconds: float = 12.0) -> dict | None:
@@ -156,6 +156,7 @@ def main():
     units_per_launch = frames * 2 * n_snr
     achieved = units_per_launch * BYTES_PER_SYMBOL_SNR / rx_avg_s / 1e9
     res = pkg.SweepResult(SNR_GRID, c)
+    pmc = load_pmc(args.workload)
     if rank == 0:
         line = {
             "metric": "OFDM symbols/sec (whole node) over BER-vs-SNR sweep; achieved HBM GB/s vs peak",
@@ -175,12 +176,21 @@ def main():
                        "parallelism": f"dp{world} (counter-range shards, 1 RCCL all-reduce)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": load_pmc_traffic(args.workload),
+                         "traffic": pmc.get("rx_hbm_bytes_per_launch"),
                          "kernel": "rx_ls_kernel" if kw["est"] == "ls" else "rx_ideal_kernel",
                          "bytes_per_unit": BYTES_PER_SYMBOL_SNR,
                          "units_per_launch": units_per_launch,
                          "avg_launch_ms": rx_avg_s * 1e3, "launches": rx_n,
-                         "achieved_loaded_GBs": units_per_launch * BYTES_LOADED_PER_SYMBOL_SNR / rx_avg_s / 1e9},
+                         "traffic_note": "HBM bytes per launch from FETCH_SIZE x2 (gfx950) + WRITE_SIZE, "
+                                         "profiles/pmc_summary.json; each symbol is staged once per launch "
+                                         "and re-used from LDS for every SNR point"},
+            # the kernel is VALU-issue bound: measured VALU wave-instructions per unit
+            # (SQ_INSTS_VALU / units, rocprofv3) x units / live launch time vs the issue peak
+            "valu_roofline": ({"achieved": units_per_launch * pmc["valu_instr_per_unit"] / rx_avg_s,
+                               "peak": VALU_PEAK_PER_S, "unit": "wave-instr/s",
+                               "frac": units_per_launch * pmc["valu_instr_per_unit"] / rx_avg_s / VALU_PEAK_PER_S,
+                               "instr_per_unit": pmc["valu_instr_per_unit"]}
+                              if pmc.get("valu_instr_per_unit") else None),
             "kernels_ms": {"rx_total": rx_ms, "rx_launches": rx_n, "tx_total": tx_ms, "tx_launches": tx_n},
             "results": {"ber": res.ber.tolist(), "evm_pre_db": res.evm_pre_db.tolist()},
         }

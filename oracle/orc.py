@@ -248,6 +248,12 @@ class RefLib:
         self.lib.ref_ifft(_p(i), _p(o), len(i))
         return o
 
+    def channel_estimation(self, frame480: np.ndarray) -> np.ndarray:
+        """Channel_Estimation (OFDM.c:830-850) on a 480-sample symbol-rate frame -> H[64]."""
+        i = np.ascontiguousarray(frame480, np.complex64); o = np.zeros(64, np.complex64)
+        self.lib.ref_channel_estimation(_p(i), _p(o))
+        return o
+
     def receiver_stages(self, ota: np.ndarray, rx_start: int):
         ota = np.ascontiguousarray(ota, np.complex64)
         nf = 2

@@ -13,6 +13,9 @@ Outputs (all plain data, loadable with numpy allow_pickle=False / json):
   matlab_output.npz    the 96 KAT bits of data/Matlab_Output.txt (MATLAB Tester RX_Payload_1_demod)
   reference_data.json  the four data/Output_*.txt files of the reference run (format fixtures)
   ref_mc_curve.json    Monte-Carlo BER/EVM of the reference's own trial loop (TOA+Receiver) per SNR
+  ref_genie_ls_curve.json  genie-timed symbol chain built from the reference's own ifft/fft/
+                       Channel_Estimation (two separately noised LTF windows), real noise
+                       sigma^2 = 0.4980 * 52/4096 / snr: pins symbol mode's LS estimator statistically
 """
 from __future__ import annotations
 
@@ -83,6 +86,55 @@ def gen_kat():
     (HERE / "reference_data.json").write_text(json.dumps(files, indent=1))
 
 
+# fftshifted data bins / pilots of the subcarrier map (OFDM.c:523-548)
+DATA_IDX = np.array([*range(6, 11), *range(12, 25), *range(26, 32), *range(33, 39), *range(40, 53), *range(54, 59)])
+PILOTS = {11: 1.0, 25: 1.0, 39: 1.0, 53: -1.0}
+
+
+def gen_genie(R: RefLib, frames: int = 20000, snrs=(0.0, 2.0, 4.0, 6.0)):
+    rng = np.random.default_rng(80211)
+    T = R.ifft(R.globals()["ltf_freq"])                       # long training symbol, C ifft (D5)
+    ltf160 = np.concatenate([T[32:], T, T])
+    s2 = 1 / np.sqrt(2)
+    rows = []
+    for snr in snrs:
+        sigma = np.sqrt(0.4980 * 52 / 4096 / 10 ** (snr / 10))
+        nbits = nerr = 0
+        epre = 0.0
+        for _ in range(frames):
+            frame = np.zeros(480, np.complex64)
+            frame[160:320] = ltf160
+            bits = rng.integers(0, 2, (2, 96))
+            for d in range(2):
+                b0, b1 = bits[d, 0::2], bits[d, 1::2]
+                # 00:(1+j) 01:(-1+j) 10:(-1-j) 11:(1-j), /sqrt2 (OFDM.c:423-430)
+                q = (np.where(b0 == b1, 1.0, -1.0) + 1j * np.where(b0 == 1, -1.0, 1.0)) * s2
+                X = np.zeros(64, np.complex64)
+                X[DATA_IDX] = q
+                for k, v in PILOTS.items():
+                    X[k] = v
+                x = R.ifft(X)
+                frame[320 + 80 * d:400 + 80 * d] = np.concatenate([x[48:], x])
+            rx = (frame + (sigma * rng.standard_normal(480)).astype(np.float32)).astype(np.complex64)  # D7
+            H = R.channel_estimation(rx)
+            for d in range(2):
+                Y = R.fft(rx[336 + 80 * d:400 + 80 * d])
+                z = Y[DATA_IDX].astype(np.complex128) / H[DATA_IDX]
+                pr, pi = z.real > 0, z.imag > 0
+                c0, c1 = (~pi).astype(int), (pr != pi).astype(int)
+                nerr += int(np.sum(c0 != bits[d, 0::2]) + np.sum(c1 != bits[d, 1::2]))
+                nbits += 96
+                b0, b1 = bits[d, 0::2], bits[d, 1::2]
+                ref = (np.where(b0 == b1, 1.0, -1.0) + 1j * np.where(b0 == 1, -1.0, 1.0)) * s2
+                epre += float(np.sum(np.abs(z - ref) ** 2))
+        rows.append({"snr_db": snr, "frames": frames, "bits": nbits, "bit_err": nerr, "evm_terms": nbits // 2,
+                     "sum_evm_pre": epre})
+    meta = {"generator": "tests/golden/gen_golden.py gen_genie",
+            "source": "reference ifft/fft/Channel_Estimation (OFDM.c:314-339, 830-850), numpy real noise",
+            "rows": rows}
+    (HERE / "ref_genie_ls_curve.json").write_text(json.dumps(meta, indent=1))
+
+
 def _mc_worker(args):
     snr, n, seed = args
     R = RefLib()
@@ -121,10 +173,14 @@ def main():
     ap.add_argument("--mc-trials", type=int, default=8000)
     ap.add_argument("--procs", type=int, default=8)
     ap.add_argument("--skip-mc", action="store_true")
+    ap.add_argument("--only", choices=["genie"], help="regenerate one fixture only")
     a = ap.parse_args()
     build_ref()
     R = RefLib()
-    gen_fft(R); gen_tx(R); gen_rx(R); gen_kat()
+    if a.only == "genie":
+        gen_genie(R)
+        return
+    gen_fft(R); gen_tx(R); gen_rx(R); gen_kat(); gen_genie(R)
     if not a.skip_mc:
         gen_mc(a.mc_trials, a.procs)
     print("golden fixtures written to", HERE)

@@ -194,3 +194,21 @@ def test_rayleigh_zf_diversity(engine, pkg):
     c = engine.symbol_sweep(cfg, [10.0, 20.0, 30.0], 200_000)
     ber = c[:, 3] / c[:, 2]
     assert 5 < ber[0] / ber[1] < 20 and 5 < ber[1] / ber[2] < 20, ber
+
+
+def test_ls_gpu_matches_reference_estimator_curve(engine, pkg):
+    """GPU LS symbol chain (1e6 frames/point) vs the reference's own Channel_Estimation on two separately
+    noised LTF windows (tests/golden/ref_genie_ls_curve.json): BER within sampling error, EVM (>= 4 dB)."""
+    import json
+    from conftest import GOLDEN
+    rows = json.loads((GOLDEN / "ref_genie_ls_curve.json").read_text())["rows"]
+    snrs = [r["snr_db"] for r in rows]
+    c = engine.symbol_sweep(pkg.make_cfg(), snrs, 1_000_000)
+    for r, row in zip(rows, c):
+        p_ref, p = r["bit_err"] / r["bits"], row[3] / row[2]
+        sd = math.sqrt(3 * p_ref / r["bits"] + 3 * p / row[2])
+        assert abs(p - p_ref) < 5 * sd, (r["snr_db"], p, p_ref)
+        if r["snr_db"] >= 4:
+            evm_ref = 10 * np.log10(r["sum_evm_pre"] / r["evm_terms"])
+            evm = 10 * np.log10(row[7] / 2 ** 20 / row[6])
+            assert abs(evm - evm_ref) < 0.05, (r["snr_db"], evm, evm_ref)

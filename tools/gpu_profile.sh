@@ -14,11 +14,10 @@ step() {
   echo "[$(date +%T)] end $name rc=$rc"; tail -3 "gpurun_out/$name.log"
   if fatal $rc; then echo "fatal rc=$rc in $name: stopping"; exit $rc; fi
 }
-BARGS=${BENCH_ARGS:---steps 1 --warmup 1 --no-cpu-baseline --symbols 2000000}
-step counters_list 120 rocprofv3 -L
+BARGS=${BENCH_ARGS:---steps 1 --warmup 1 --no-cpu-baseline}
 step trace 300 rocprofv3 --kernel-trace --stats -d gpurun_out/pmc_trace -o run --output-format csv -- python3 bench.py $BARGS
 i=0
-for grp in ${PMC_GROUPS:-"FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_SALU" "GRBM_GUI_ACTIVE GRBM_COUNT" "TCC_HIT_sum TCC_MISS_sum"}; do
+for grp in ${PMC_GROUPS:-"FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_SALU" "GRBM_GUI_ACTIVE GRBM_COUNT" "TCC_HIT_sum TCC_MISS_sum" "SQ_INSTS_VALU_TRANS_F SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_VALU_FMA_F"}; do
   i=$((i+1))
   step pmc_$i 300 rocprofv3 --pmc $grp -d gpurun_out/pmc_$i -o run --output-format csv -- python3 bench.py $BARGS
 done
