@@ -136,31 +136,51 @@ __global__ __launch_bounds__(256, 3) void tx_symbols_kernel(TxArgs a) {
 }
 
 // ======================================================================== K3: receiver chain
-// Where the clean samples of a lane's window come from.  Both sources index sample n (-3..63,
+// Where the clean samples of a lane's window come from: sample n (-3..63,
 // negative = cyclic prefix, reached only by the 4-tap channel) with a compile-time offset.
-// GlobalRows: sample n of symbol s at row16[n * pitch + s] (row-major batch, wave-uniform row base,
-// so loads use saddr + one per-lane offset).
-struct GlobalRows {
-    const float2 *row16;
-    int64_t pitch;
-    uint32_t s;
-    __device__ __forceinline__ void fresh() {
-        // uniform operands too: otherwise all 64 row addresses are hoisted into SGPRs and spill
-        asm volatile("" : "+s"(row16), "+s"(pitch));
-        opaque(s);
-    }
-    template <int N>
-    __device__ __forceinline__ float2 at() const { return gld((gcf2 *)(row16 + N * pitch), (int)s); }
-};
-// LdsRows: the LS receiver's staged group, LS_ROW_F2 float2 per row starting at sample R0 - 16;
-// base = this lane's column (a data symbol, or the 2T column for the LTF-pair lane).
-template <int R0>
+// LdsRows: a staged group in LDS (StageGeom), ROW_F2 float2 per row starting at sample R0 - 16;
+// base = this lane's column (a data symbol, or the LS receiver's 2T column for the LTF-pair lane).
+template <int R0, int ROW_F2>
 struct LdsRows {
     lcf2 *base;
     __device__ __forceinline__ void fresh() { opaque(base); }
     template <int N>
-    __device__ __forceinline__ float2 at() const { return ld2(base, (N + 16 - R0) * LS_ROW_F2); }
+    __device__ __forceinline__ float2 at() const { return ld2(base, (N + 16 - R0) * ROW_F2); }
 };
+
+// A staged group in LDS: rows R0..79 (R0 = 12 when the 4-tap channel reaches into the CP), each row
+// DATA_CHUNKS x 16 B of consecutive symbols followed by EXTRA_CHUNKS x 16 B from a per-row table
+// (the LS receiver's 2T column).
+template <int CHAN, int DATA_CHUNKS, int EXTRA_CHUNKS>
+struct StageGeom {
+    static constexpr int R0 = CHAN == OFDM_CHAN_RAYLEIGH4 ? 12 : 16;
+    static constexpr int ROWS = SYM_SAMPLES - R0;
+    static constexpr int DATA = DATA_CHUNKS;
+    static constexpr int ROW_CHUNKS = DATA_CHUNKS + EXTRA_CHUNKS;
+    static constexpr int ROW_F2 = 2 * ROW_CHUNKS;
+    static constexpr int CHUNKS = ROWS * ROW_CHUNKS;
+    static constexpr int BUF_F2 = ROWS * ROW_F2;
+};
+
+// HBM -> LDS by LDS-DMA (global_load_lds_dwordx4: 1 KB per wave-instruction, chunk c lands at LDS
+// byte 16 c), spread over the block's 4 waves.  `extra` holds 16 B per table row, row r = window
+// sample r - 4 (so staged row `row` uses table row row + R0 - 12).
+template <typename G>
+__device__ __forceinline__ void stage_group(const RxArgs &a, int64_t col0, float2 *buf, const float2 *extra, int wv,
+                                            int lane) {
+    const float2 *c0 = a.tx + col0;
+    for (int k = wv; k * 64 < G::CHUNKS; k += 4) {
+        const int c = k * 64 + lane;
+        if (c < G::CHUNKS) {
+            const int row = c / G::ROW_CHUNKS, j = c - row * G::ROW_CHUNKS;
+            const char *src = j < G::DATA ? (const char *)(c0 + (int64_t)(G::R0 + row) * a.pitch) + j * 16
+                                          : (const char *)(extra + 2 * (row + G::R0 - 12));
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)src,
+                                             (__attribute__((address_space(3))) void *)((char *)buf + k * 1024),
+                                             16, 0, 0);
+        }
+    }
+}
 
 // Load + channel + AWGN for samples n0..n0+3, times (-1)^n (fft() = DFT of x(-1)^n, OFDM.c:314-318).
 // Noise sample at frame time t uses Gaussian t (real) or 2t, 2t+1 (complex) of the frame's stream
@@ -261,32 +281,8 @@ __device__ __forceinline__ void finish_symbol(float2 (&x)[64], const uint32_t (&
 // The 4 waves of a block share one staged group (42 symbols x 64-68 rows, plus the 2T column)
 // in LDS and split the SNR points; the next group is prefetched by LDS-DMA into the other buffer.
 template <int CHAN>
-struct LsGroup {
-    static constexpr int R0 = CHAN == OFDM_CHAN_RAYLEIGH4 ? 12 : 16;   // first staged sample row
-    static constexpr int ROWS = SYM_SAMPLES - R0;
-    static constexpr int ROW_CHUNKS = LS_ROW_F2 / 2;                  // 16-B chunks per staged row
-    static constexpr int CHUNKS = ROWS * ROW_CHUNKS;
-    static constexpr int BUF_F2 = ROWS * LS_ROW_F2;
-    static_assert(LS_GROUP_SYMS / 2 + 1 == ROW_CHUNKS, "42 data symbols + one 2T chunk per row");
-};
-
-template <int CHAN>
-__device__ __forceinline__ void ls_stage(const RxArgs &a, int64_t grp, float2 *buf, int wv, int lane) {
-    using G = LsGroup<CHAN>;
-    const float2 *col0 = a.tx + grp * LS_GROUP_SYMS;
-    for (int k = wv; k * 64 < G::CHUNKS; k += 4) {
-        const int c = k * 64 + lane;                    // chunk c lands at LDS byte 16 c (M0 + 16 lane)
-        if (c < G::CHUNKS) {
-            const int row = c / G::ROW_CHUNKS, j = c - row * G::ROW_CHUNKS;
-            const char *src = j < LS_GROUP_SYMS / 2
-                ? (const char *)(col0 + (int64_t)(G::R0 + row) * a.pitch) + j * 16
-                : (const char *)(a.ltf2_rows + 2 * (row + G::R0 - 12));
-            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)src,
-                                             (__attribute__((address_space(3))) void *)((char *)buf + k * 1024),
-                                             16, 0, 0);
-        }
-    }
-}
+using LsGeom = StageGeom<CHAN, LS_GROUP_SYMS / 2, 1>;      // 42 data symbols + the 2T chunk per row
+static_assert(LS_ROW_F2 == 2 * (LS_GROUP_SYMS / 2 + 1), "LS staged row = 42 symbols + 2T (x2)");
 
 template <int BIN>
 __device__ __forceinline__ EqOut<2> ls_equalise_bp(float2 Y, uint32_t e_addr) {
@@ -301,7 +297,7 @@ __device__ __forceinline__ EqOut<2> ls_equalise_bp(float2 Y, uint32_t e_addr) {
 
 template <int NOISE, int CHAN, bool DUMP>
 __global__ __launch_bounds__(256, OFDM_RX_LS_WAVES) void rx_ls_kernel(RxArgs a) {
-    using G = LsGroup<CHAN>;
+    using G = LsGeom<CHAN>;
     __shared__ unsigned long long sacc[OFDM_MAX_SNR][8];
     __shared__ __attribute__((aligned(16))) float2 sbuf[2][G::BUF_F2];
     for (int i = threadIdx.x; i < a.n_snr * 8; i += blockDim.x) (&sacc[0][0])[i] = 0ull;
@@ -319,7 +315,7 @@ __global__ __launch_bounds__(256, OFDM_RX_LS_WAVES) void rx_ls_kernel(RxArgs a) 
 
     int cur = 0;
     int64_t grp = blockIdx.x;
-    if (grp < n_groups) ls_stage<CHAN>(a, grp, sbuf[0], wv, lane);
+    if (grp < n_groups) stage_group<G>(a, grp * LS_GROUP_SYMS, sbuf[0], a.ltf2_rows, wv, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (; grp < n_groups; grp += gridDim.x) {
@@ -337,12 +333,12 @@ __global__ __launch_bounds__(256, OFDM_RX_LS_WAVES) void rx_ls_kernel(RxArgs a) 
         float2 h[4] = {make_float2(1.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f)};
         if constexpr (CHAN == OFDM_CHAN_RAYLEIGH4) channel_taps(f_lo, f_hi, a.k0, a.k1, h);
         const int64_t nxt = grp + gridDim.x;
-        if (nxt < n_groups) ls_stage<CHAN>(a, nxt, sbuf[cur ^ 1], wv, lane);
-        LdsRows<G::R0> src;
+        if (nxt < n_groups) stage_group<G>(a, nxt * LS_GROUP_SYMS, sbuf[cur ^ 1], a.ltf2_rows, wv, lane);
+        LdsRows<G::R0, G::ROW_F2> src;
         src.base = (lcf2 *)(sbuf[cur] + col);
 
         for (int q = wv; q < a.n_snr; q += 4) {
-            LdsRows<G::R0> s = src;
+            LdsRows<G::R0, G::ROW_F2> s = src;
             uint32_t wq[3] = {w[0], w[1], w[2]};
             uint32_t flo = f_lo, fhi = f_hi;
             float2 hq[4] = {h[0], h[1], h[2], h[3]};
@@ -373,34 +369,37 @@ __global__ __launch_bounds__(256, OFDM_RX_LS_WAVES) void rx_ls_kernel(RxArgs a) 
     block_flush(a, sacc);
 }
 
-// ---- ideal channel knowledge: every lane a data symbol; wave = 64 consecutive symbols ----
+// ---- ideal channel knowledge: every lane a data symbol ----
+// A block stages 64 consecutive symbols (rows R0..79, 32-34 KB, one buffer: three blocks per CU hide
+// each other's staging) and its 4 waves split the SNR points over them.
 template <int CONV, int NOISE, int CHAN, bool DUMP>
 __global__ __launch_bounds__(256, OFDM_RX_IDEAL_WAVES) void rx_ideal_kernel(RxArgs a) {
+    using G = StageGeom<CHAN, 32, 0>;
     __shared__ unsigned long long sacc[OFDM_MAX_SNR][8];
+    __shared__ __attribute__((aligned(16))) float2 sbuf[G::BUF_F2];
     for (int i = threadIdx.x; i < a.n_snr * 8; i += blockDim.x) (&sacc[0][0])[i] = 0ull;
-    __syncthreads();
     const int lane = threadIdx.x & 63;
-    const int64_t wave_id = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    const int64_t n_waves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    const int wv = threadIdx.x >> 6;
     const int d = lane & 1;
     const uint32_t t0 = 336u + 80u * (uint32_t)d;
-    const int64_t n_sym = 2 * a.n_frames;
+    const int64_t n_groups = (2 * a.n_frames + 63) / 64;
     const int64_t P = a.pitch;
-    for (int64_t wg = wave_id; wg * 64 < n_sym; wg += n_waves) {
-        const uint32_t so = (uint32_t)(wg * 64 + lane);
+    for (int64_t grp = blockIdx.x; grp < n_groups; grp += gridDim.x) {
+        stage_group<G>(a, grp * 64, sbuf, nullptr, wv, lane);
+        const uint32_t so = (uint32_t)(grp * 64 + lane);
         const int64_t fl = (int64_t)(so >> 1);
         const bool valid = fl < a.n_frames;
         const uint64_t f = a.first_frame + (uint64_t)fl;
         const uint32_t f_lo = (uint32_t)f, f_hi = (uint32_t)(f >> 32);
-        GlobalRows src;
-        src.row16 = a.tx + 16 * P;
-        src.pitch = P;
-        src.s = so;
         uint32_t w[3] = {a.bits[so], a.bits[P + so], a.bits[2 * P + so]};
         float2 h[4] = {make_float2(1.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f)};
         if constexpr (CHAN == OFDM_CHAN_RAYLEIGH4) channel_taps(f_lo, f_hi, a.k0, a.k1, h);
-        for (int q = 0; q < a.n_snr; ++q) {
-            GlobalRows s = src;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();                                   // the group has landed for every wave
+        LdsRows<G::R0, G::ROW_F2> src;
+        src.base = (lcf2 *)(sbuf + lane);
+        for (int q = wv; q < a.n_snr; q += 4) {
+            LdsRows<G::R0, G::ROW_F2> s = src;
             uint32_t wq[3] = {w[0], w[1], w[2]};
             uint32_t flo = f_lo, fhi = f_hi;
             float2 hq[4] = {h[0], h[1], h[2], h[3]};
@@ -439,6 +438,7 @@ __global__ __launch_bounds__(256, OFDM_RX_IDEAL_WAVES) void rx_ideal_kernel(RxAr
             auto partner = [](uint32_t v) { return dpp_u<DPP_QUAD_XOR1>(v); };
             finish_symbol<DUMP, KIND>(x, wq, Hof, partner, dump_eq, dump_bits, d == 0 && valid, sacc[q]);
         }
+        __syncthreads();                                   // every wave is done with the group
     }
     block_flush(a, sacc);
 }
@@ -497,8 +497,9 @@ void launch_rx(hipStream_t st, const RxArgs &a, const ofdm_cfg &cfg, bool dump, 
 
 int rx_grid(const ofdm_cfg &cfg, int64_t n_frames, int device) {
     // LS: one block per 21-frame group in flight; ideal: one wave per 64 symbols, 4 waves per block
+    // one block per staged group in flight (LS: 21 frames, ideal: 64 symbols)
     const int64_t need = cfg.est == OFDM_EST_LS ? (n_frames + LS_GROUP_FRAMES - 1) / LS_GROUP_FRAMES
-                                                : ((2 * n_frames + 63) / 64 + 3) / 4;
+                                                : (2 * n_frames + 63) / 64;
     int per_cu = 0, cus = 0;
     const void *k = cfg.est == OFDM_EST_LS
         ? (cfg.channel == OFDM_CHAN_AWGN

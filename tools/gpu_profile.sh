@@ -16,9 +16,13 @@ step() {
 }
 BARGS=${BENCH_ARGS:---steps 1 --warmup 1 --no-cpu-baseline}
 step trace 300 rocprofv3 --kernel-trace --stats -d gpurun_out/pmc_trace -o run --output-format csv -- python3 bench.py $BARGS
+# counter groups, ';'-separated (one rocprofv3 --pmc pass each)
+GROUPS_DEFAULT="FETCH_SIZE;WRITE_SIZE;SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_SALU;GRBM_GUI_ACTIVE GRBM_COUNT;TCC_HIT_sum TCC_MISS_sum;SQ_INSTS_VALU_TRANS_F SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_VALU_FMA_F"
+IFS=';' read -r -a GROUPS_ARR <<< "${PMC_GROUPS:-$GROUPS_DEFAULT}"
 i=0
-for grp in ${PMC_GROUPS:-"FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_SALU" "GRBM_GUI_ACTIVE GRBM_COUNT" "TCC_HIT_sum TCC_MISS_sum" "SQ_INSTS_VALU_TRANS_F SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_VALU_FMA_F"}; do
+for grp in "${GROUPS_ARR[@]}"; do
   i=$((i+1))
+  # shellcheck disable=SC2086
   step pmc_$i 300 rocprofv3 --pmc $grp -d gpurun_out/pmc_$i -o run --output-format csv -- python3 bench.py $BARGS
 done
 echo "profile session done"
