@@ -8,6 +8,7 @@ data/Output_*.txt file surface.  There is no CPU fallback.
 from . import abi  # noqa: F401
 from .abi import OfdmError, load_library, make_cfg, make_rx_opts  # noqa: F401
 from .engine import Engine, SweepResult  # noqa: F401
-from .fileio import read_float_array_file, write_float_array_to_file, write_reference_outputs  # noqa: F401
+from .fileio import (decode_message, read_float_array_file, write_bits_file,  # noqa: F401
+                     write_float_array_to_file, write_reference_outputs)
 
 __version__ = "0.1.0"

@@ -25,7 +25,8 @@ CHANNEL = {"awgn": 0, "rayleigh4": 1}
 # counters
 NCOUNTERS = 16
 C_FRAMES, C_SYMBOLS, C_BITS, C_BIT_ERR, C_FRAME_ERR, C_SYNC_FAIL, C_EVM_TERMS, C_EVM_PRE_Q, \
-    C_EVM_POST_AXIS, C_EVMDB_PRE_Q, C_EVMDB_POST_Q, C_EVMDB_POST_FINITE, C_OOB = range(13)
+    C_EVM_POST_AXIS, C_EVMDB_PRE_Q, C_EVMDB_POST_Q, C_EVMDB_POST_FINITE, C_OOB, \
+    C_WL_MIN_Q, C_WL_MAX_Q, C_WL_BITS = range(16)
 EVM_Q_SCALE = float(1 << 20)
 
 # kernel ids for timing
@@ -50,9 +51,12 @@ _SIGS = {
     "ofdm_rx_frames": (C.c_int, [_V, _V, _V, _V, C.c_uint64, C.c_int64, _V, C.c_int, _V]),
     "ofdm_rx_frames_dump": (C.c_int, [_V, _V, _V, _V, C.c_uint64, C.c_int64, _V, C.c_int, _V, _V, _V]),
     "ofdm_symbol_sweep": (C.c_int, [_V, _V, _V, C.c_int, C.c_uint64, C.c_int64, C.c_int64, _V]),
+    "ofdm_set_message": (C.c_int, [_V, C.c_char_p, C.c_int32, C.POINTER(C.c_int32)]),
+    "ofdm_payload_frames": (C.c_int, [_V, C.c_int, C.POINTER(C.c_int32)]),
     "ofdm_transmitter": (C.c_int, [_V, C.c_int, C.c_int, C.c_int, _V, C.c_int32, C.POINTER(C.c_int32)]),
     "ofdm_transmission_over_air": (C.c_int, [_V, _V, _V, C.c_int32, C.c_double, C.c_uint64, C.c_uint64, C.c_int32]),
     "ofdm_receiver": (C.c_int, [_V, _V, _V, C.c_int, _V, _V, _V, _V]),
+    "ofdm_word_length_report": (C.c_int, [_V, _V, C.c_int32, _V, C.POINTER(C.c_int32)]),
     "ofdm_frame_sweep": (C.c_int, [_V, _V, _V, _V, C.c_int, C.c_uint64, C.c_int64, _V, _V]),
 }
 EXPORTS = tuple(_SIGS)
@@ -72,7 +76,8 @@ class Cfg(C.Structure):
 class RxOpts(C.Structure):
     """ofdm_rx_opts"""
     _fields_ = [("cap_len", C.c_int32), ("float_cfo", C.c_int32), ("matlab_slicer", C.c_int32),
-                ("float_taps", C.c_int32), ("fixed_start", C.c_int32), ("reserved", C.c_int32 * 3)]
+                ("float_taps", C.c_int32), ("fixed_start", C.c_int32), ("word_stats", C.c_int32),
+                ("reserved", C.c_int32 * 2)]
 
 
 def make_cfg(seed: int = 0x80211A, conv: str = "c", payload: str = "random", est: str = "ls",
@@ -81,11 +86,21 @@ def make_cfg(seed: int = 0x80211A, conv: str = "c", payload: str = "random", est
     return Cfg(seed, CONV[conv], PAYLOAD[payload], EST[est], NOISE[noise], CHANNEL[channel], 2, kappa, p_ref)
 
 
+def wave_len(frames: int) -> int:
+    """Transmitter() output length for `frames` data symbols (OFDM.c:569-612): 10 x (2 (320 + 80 D) + 20)."""
+    return 10 * (2 * (320 + 80 * frames) + 20)
+
+
+def capture_len(frames: int) -> int:
+    """Receiver() capture, int(0.307 x waveform length) (OFDM.c:945): 3008 for D = 2."""
+    return int(wave_len(frames) * 0.307)
+
+
 def make_rx_opts(mode: str = "c", fixed_start: int = -1) -> RxOpts:
-    """mode 'c': OFDM.c receiver (capture 3008 = floor(0.307*9800), fp32 CFO, fp32 taps);
-    'matlab': IEEE_802_11_a_Code_Tester.m (capture 3000, MATLAB slicer, double taps)."""
+    """mode 'c': OFDM.c receiver (capture int(0.307 len), 3008 for the reference message; fp32 CFO,
+    fp32 taps); 'matlab': IEEE_802_11_a_Code_Tester.m (capture 3000, MATLAB slicer, double taps)."""
     if mode == "c":
-        return RxOpts(3008, 1, 0, 1, fixed_start)
+        return RxOpts(0, 1, 0, 1, fixed_start)
     if mode == "matlab":
         return RxOpts(3000, 0, 1, 0, fixed_start)
     raise ValueError(mode)

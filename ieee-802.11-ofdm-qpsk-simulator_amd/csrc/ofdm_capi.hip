@@ -49,19 +49,23 @@ static void host_ltf_time(int conv, std::vector<float2> &out) {
 }
 
 // payload words: reference message (Data_Generator, OFDM.c:435-465) or MATLAB Tester (Tester.m:50-51)
-void payload_table(int payload, uint32_t table[6]) {
-    unsigned char bytes[24];
-    if (payload == OFDM_PAYLOAD_TESTER) {
+int payload_table(int payload, const std::string &message, uint32_t table[3 * MSG_MAX_FRAMES]) {
+    unsigned char bytes[MSG_MAX_CHARS];
+    int frames;
+    if (payload == OFDM_PAYLOAD_TESTER) {                       // 'A' x 11 + ' ' per 96 bits (Tester.m:50-51)
+        frames = 2;
         for (int f = 0; f < 2; ++f)
             for (int c = 0; c < 12; ++c) bytes[12 * f + c] = c < 11 ? 0x41 : 0x20;
     } else {
-        static const char msg[] = "Hey! I am Vivaswan";          // OFDM.c:20
-        const int len = (int)sizeof(msg) - 1;
-        for (int c = 0; c < 24; ++c) bytes[c] = c < len ? (unsigned char)msg[c] : ' ';
+        const int len = (int)message.size();
+        frames = (8 * len + 95) / 96;                           // ceil(8 len / 96) (OFDM.c:439)
+        for (int c = 0; c < 12 * frames; ++c) bytes[c] = c < len ? (unsigned char)message[c] : ' ';
     }
-    for (int w = 0; w < 6; ++w)
+    for (int w = 0; w < 3 * frames; ++w)
         table[w] = ((uint32_t)bytes[4 * w] << 24) | ((uint32_t)bytes[4 * w + 1] << 16) |
                    ((uint32_t)bytes[4 * w + 2] << 8) | (uint32_t)bytes[4 * w + 3];
+    for (int w = 3 * frames; w < 3 * MSG_MAX_FRAMES; ++w) table[w] = 0u;
+    return frames;
 }
 
 int check_cfg(const ofdm_cfg *c) {
@@ -212,6 +216,28 @@ int ofdm_ctx_synchronize(ofdm_ctx *ctx) {
     return OFDM_OK;
 }
 
+int ofdm_set_message(ofdm_ctx *ctx, const char *msg, int32_t len, int32_t *frames) {
+    Ctx *c = reinterpret_cast<Ctx *>(ctx);
+    if (!c || (len && !msg)) return set_error(OFDM_E_ARG, "bad message arguments");
+    if (len < 1 || len > MSG_MAX_CHARS)
+        return set_error(OFDM_E_ARG, "message length %d outside [1, %d] (at most %d data symbols per frame)", len,
+                         MSG_MAX_CHARS, MSG_MAX_FRAMES);
+    c->message.assign(msg, (size_t)len);
+    c->wave_key = -1;                                          // the frame waveform depends on it
+    if (frames) *frames = (8 * len + 95) / 96;
+    return OFDM_OK;
+}
+
+int ofdm_payload_frames(ofdm_ctx *ctx, int payload, int32_t *frames) {
+    Ctx *c = reinterpret_cast<Ctx *>(ctx);
+    if (!c || !frames) return set_error(OFDM_E_ARG, "bad arguments");
+    if (payload != OFDM_PAYLOAD_MESSAGE && payload != OFDM_PAYLOAD_TESTER)
+        return set_error(OFDM_E_ARG, "payload %d has no fixed frame structure", payload);
+    uint32_t t[3 * MSG_MAX_FRAMES];
+    *frames = payload_table(payload, c->message, t);
+    return OFDM_OK;
+}
+
 int ofdm_timing_enable(ofdm_ctx *ctx, int enable) {
     Ctx *c = reinterpret_cast<Ctx *>(ctx);
     if (!c) return set_error(OFDM_E_ARG, "ctx is NULL");
@@ -279,7 +305,7 @@ int ofdm_tx_frames(ofdm_ctx *ctx, const ofdm_cfg *cfg, uint64_t first_frame, int
     a.k0 = (uint32_t)cfg->seed;
     a.k1 = (uint32_t)(cfg->seed >> 32);
     a.payload = cfg->payload;
-    payload_table(cfg->payload, a.table);
+    a.table_frames = payload_table(cfg->payload, c->message, a.table);
     c->tic(Ctx::K_TX);
     launch_tx(c->stream, a, cfg->conv);
     c->toc();

@@ -10,7 +10,12 @@ namespace ofdm {
 
 int set_error(int code, const char *fmt, ...);
 int check_cfg(const ofdm_cfg *c);
-void payload_table(int payload, uint32_t table[6]);
+
+constexpr int MSG_MAX_FRAMES = 8;           // data symbols per frame-mode frame (LDS budget)
+constexpr int MSG_MAX_CHARS = 12 * MSG_MAX_FRAMES;
+// payload words (MSB-first bits, 3 per data symbol) of the TESTER pattern or `message` padded with
+// ' ' to whole symbols (Data_Generator, OFDM.c:435-465); returns the data symbols per frame
+int payload_table(int payload, const std::string &message, uint32_t table[3 * MSG_MAX_FRAMES]);
 
 struct Ctx {
     enum { K_FFT = 0, K_TX = 1, K_RX = 2, K_FRAME = 3, NK = 4 };
@@ -20,12 +25,14 @@ struct Ctx {
     hipStream_t stream = nullptr;    // where work is enqueued (own or external)
     float2 *d_ltf[2] = {nullptr, nullptr};
     float2 *d_ltf2_rows[2] = {nullptr, nullptr};   // LS staging column: [68][2] 2T[(r - 4) mod 64]
+    std::string message = "Hey! I am Vivaswan";   // MESSAGE payload (OFDM.c:20), ofdm_set_message
     // sweep scratch (grown on demand, freed with the context)
     void *d_tx = nullptr, *d_bits = nullptr, *d_cnt = nullptr, *d_scratch = nullptr, *d_scratch2 = nullptr;
     void *d_wave = nullptr;
     size_t cap_tx = 0, cap_bits = 0, cap_cnt = 0, cap_scratch = 0, cap_scratch2 = 0, cap_wave = 0;
-    // frame-mode waveform cache (per conv/payload/taps)
+    // frame-mode waveform cache (per conv/payload/message)
     int wave_key = -1;
+    int wave_frames = 0;
     int32_t wave_len = 0;
     double wave_power = 0.0;
     // kernel timing

@@ -4,30 +4,32 @@
 //                           stuffing, 21-tap RRC, x10 repeat, mean power (OFDM.c:637-643).
 //   K4b frame_rx_kernel   : one wave per trial: capture (OFDM.c:945-955) + real AWGN (OFDM.c:651),
 //                           Packet_Detection (659-683) with sliding sums, Packet_Selection (685-771)
-//                           as a wave ballot/min, RRC matched filter evaluated only at the 480
+//                           as a wave ballot/min, RRC matched filter evaluated only at the 320+80D
 //                           down-sampled instants (965, 984-996), coarse/fine CFO (773-828), then the
 //                           same register FFT + LS estimate + demap as symbol mode (830-1165).
 //   K4c ota_kernel        : Transmission_Over_Air() on a caller-provided waveform.
 //
-// The capture lives in LDS (24 KB per wave); detection keeps only the >0.75 crossings as a bit
-// mask, since Packet_Selection needs nothing else (it re-reads Corr_Out only at front+230).
+// The capture lives in LDS (24 KB per wave for the reference's 2-symbol message; frames carry 1..8
+// data symbols, ofdm_set_message); detection keeps only the >0.75 crossings as a bit mask, since
+// Packet_Selection needs nothing else (it re-reads Corr_Out only at front+230).
 #include "ofdm_internal.h"
-#include "ofdm_rxcommon.h"
 #include "ofdm_ctx.h"
+#include "ofdm_rxcommon.h"
 #include <cmath>
 #include <cstring>
 #include <vector>
 
 namespace ofdm {
 
-constexpr int FR_SAMPLES = 480;              // 160 STF + 160 LTF + 2 x 80 data (OFDM.c:569)
-constexpr int FR_OS = 2 * FR_SAMPLES;        // 2x zero-stuffed (OFDM.c:587-595)
-constexpr int FR_FILT = FR_OS + 20;          // + 20 RRC tail (OFDM.c:603-605)
+// frame geometry for nd data symbols (OFDM.c:569-612, 945): [STF 160 | LTF 160 | nd x 80]
+constexpr int FR_MAX_DATA = MSG_MAX_FRAMES;
+constexpr int FR_MAX = 320 + 80 * FR_MAX_DATA;
 constexpr int FR_REPS = 10;                  // OFDM.c:607-612
-constexpr int WAVE_LEN = FR_FILT * FR_REPS;  // 9800
-constexpr int CAP_MAX = 3008;                // floor(0.307 * 9800) (OFDM.c:945)
-constexpr int CHUNK = 47;                    // detection positions per lane: ceil(2961 / 64)
 constexpr double TS = 1.0 / 20e6;            // OFDM.c:16-17
+__host__ __device__ constexpr int fr_len(int nd) { return 320 + 80 * nd; }
+__host__ __device__ constexpr int wave_len_for(int nd) { return (2 * fr_len(nd) + 20) * FR_REPS; }   // 2x + RRC tail
+inline int cap_len_for(int nd) { return (int)(wave_len_for(nd) * 0.307); }                          // OFDM.c:945
+constexpr int CAP_ABS_MAX = 6000;            // LDS budget of the capture (>= cap_len_for(FR_MAX_DATA) = 5955)
 
 // short training tones S_k at bins 6..58 (OFDM.c:483-490): +-1 on every 4th tone, times (1+j)
 __host__ __device__ constexpr int stf_sign(int bin) {
@@ -37,9 +39,10 @@ __host__ __device__ constexpr int stf_sign(int bin) {
 }
 
 struct WaveArgs {
-    float2 *wave;        // [WAVE_LEN]
+    float2 *wave;        // [wave_len_for(n_data)]
     double *power;       // mean |x|^2 over the waveform
-    uint32_t table[6];   // payload words of the 2 data symbols
+    uint32_t table[3 * FR_MAX_DATA];   // payload words of the data symbols
+    int32_t n_data;
     float taps[21];
     float stf_scale;     // sqrt(13/6) as the float of OFDM.c:479
 };
@@ -50,18 +53,18 @@ struct FrameArgs {
     uint64_t first_trial;
     int64_t n_trials;
     int32_t n_snr, q_base;
-    int32_t cap_len, float_cfo, matlab, fixed_start, noise, wave_len;
+    int32_t cap_len, float_cfo, matlab, fixed_start, noise, wave_len, n_data, word_stats;
     uint32_t k0, k1;
-    uint32_t table[6];
+    uint32_t table[3 * FR_MAX_DATA];
     unsigned long long *counters;   // [n_snr][OFDM_NCOUNTERS]
     int32_t *pidx_out;              // [n_snr][n_trials] or null
     // per-trial debug outputs of item 0 (ofdm_receiver), all optional
     float *dbg_res;                 // EVM_dB pre, EVM_dB post, BER
     int32_t *dbg_ints;              // packet_idx, sync_fail, oob, rx_start
-    uint32_t *dbg_bits;             // 6 words (2 symbols x 96 bits, MSB first)
-    float2 *dbg_eq;                 // 2 x 48 equalised subcarriers
+    uint32_t *dbg_bits;             // 3 words (96 bits, MSB first) per data symbol
+    float2 *dbg_eq;                 // 48 equalised subcarriers per data symbol
     float *dbg_corr;                // Corr_Out (cap_len - 47)
-    float2 *dbg_frame;              // 480 samples after fine CFO
+    float2 *dbg_frame;              // fr_len(n_data) samples after fine CFO
     float taps[21];
     float sigma[OFDM_MAX_SNR];
 };
@@ -69,12 +72,14 @@ struct FrameArgs {
 // ======================================================================== K4a: waveform
 template <int CONV>
 __global__ __launch_bounds__(256) void frame_wave_kernel(WaveArgs a) {
-    __shared__ float2 T[4][64];          // STF, LTF, D0, D1 time symbols
-    __shared__ float2 fr[FR_SAMPLES];
+    __shared__ float2 T[2 + FR_MAX_DATA][64];   // STF, LTF, data time symbols
+    __shared__ float2 fr[FR_MAX];
     __shared__ double red[256];
     const int tid = threadIdx.x;
-    if (tid < 4) {
-        const uint32_t w[3] = {a.table[3 * (tid & 1)], a.table[3 * (tid & 1) + 1], a.table[3 * (tid & 1) + 2]};
+    const int nfr = fr_len(a.n_data), nos = 2 * nfr, nfilt = nos + 20;
+    if (tid < 2 + a.n_data) {
+        const int ds = tid < 2 ? 0 : tid - 2;
+        const uint32_t w[3] = {a.table[3 * ds], a.table[3 * ds + 1], a.table[3 * ds + 2]};
         float2 X[64];
         static_for<0, 64>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
@@ -93,9 +98,9 @@ __global__ __launch_bounds__(256) void frame_wave_kernel(WaveArgs a) {
         });
     }
     __syncthreads();
-    // frame = [S(160) L(160) D1(80) D2(80)] (OFDM.c:569-583); short = first 16 samples x10,
+    // frame = [S(160) L(160) D_0(80) .. D_{nd-1}(80)] (OFDM.c:569-583); short = first 16 samples x10,
     // long = [T(32:64) T T] (Preamble_Generator, OFDM.c:392-398), data = [x(48:64) x] (559-565)
-    for (int n = tid; n < FR_SAMPLES; n += blockDim.x) {
+    for (int n = tid; n < nfr; n += blockDim.x) {
         float2 v;
         if (n < 160) v = T[0][n & 15];
         else if (n < 320) v = T[1][(n - 160 + 32) & 63];
@@ -107,19 +112,19 @@ __global__ __launch_bounds__(256) void frame_wave_kernel(WaveArgs a) {
     }
     __syncthreads();
     double pw = 0.0;
-    for (int k = tid; k < FR_FILT; k += blockDim.x) {
+    for (int k = tid; k < nfilt; k += blockDim.x) {
         // Convolution(oversampled frame, RRC) (OFDM.c:342-364); odd taps of the zero-stuffed input vanish
         float2 acc = make_float2(0.f, 0.f);
 #pragma unroll
         for (int j = 0; j < 21; ++j) {
             const int m = k - j;
-            if (m >= 0 && m < FR_OS && !(m & 1)) {
+            if (m >= 0 && m < nos && !(m & 1)) {
                 const float2 x = fr[m >> 1];
                 acc.x = fmaf(a.taps[j], x.x, acc.x);
                 acc.y = fmaf(a.taps[j], x.y, acc.y);
             }
         }
-        for (int r = 0; r < FR_REPS; ++r) a.wave[k + r * FR_FILT] = acc;
+        for (int r = 0; r < FR_REPS; ++r) a.wave[k + r * nfilt] = acc;
         pw += (double)acc.x * acc.x + (double)acc.y * acc.y;
     }
     red[tid] = pw;
@@ -128,7 +133,7 @@ __global__ __launch_bounds__(256) void frame_wave_kernel(WaveArgs a) {
         if (tid < s) red[tid] += red[tid + s];
         __syncthreads();
     }
-    if (tid == 0) *a.power = red[0] / FR_FILT;    // mean over 10 identical repeats
+    if (tid == 0) *a.power = red[0] / nfilt;      // mean over 10 identical repeats
 }
 
 // ======================================================================== K4c: over the air
@@ -187,6 +192,45 @@ __device__ __forceinline__ int wave_min_i(int v) {
     return v;
 }
 
+__device__ __forceinline__ float wave_min_f(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ float wave_max_f(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// Word_Optimization_Analysis of one capture (OFDM.c:38-73): RRC matched filter over all n + 20
+// outputs (Convolution, OFDM.c:342-364), min / max of the real and imaginary parts -> out[0..1]
+__global__ __launch_bounds__(256) void word_length_kernel(const float2 *x, int n, FrameArgs a, float *out) {
+    __shared__ float smin[4], smax[4];
+    float mn = 1e9f, mx = -1e9f;
+    for (int k = threadIdx.x; k < n + 20; k += blockDim.x) {
+        float2 v = make_float2(0.f, 0.f);
+#pragma unroll
+        for (int j = 0; j < 21; ++j) {
+            const int m = k - j;
+            if (m >= 0 && m < n) {
+                v.x = fmaf(x[m].x, a.taps[j], v.x);
+                v.y = fmaf(x[m].y, a.taps[j], v.y);
+            }
+        }
+        mn = fminf(mn, fminf(v.x, v.y));
+        mx = fmaxf(mx, fmaxf(v.x, v.y));
+    }
+    mn = wave_min_f(mn);
+    mx = wave_max_f(mx);
+    if ((threadIdx.x & 63) == 0) { smin[threadIdx.x >> 6] = mn; smax[threadIdx.x >> 6] = mx; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        out[0] = fminf(fminf(smin[0], smin[1]), fminf(smin[2], smin[3]));
+        out[1] = fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3]));
+    }
+}
+
 __device__ __forceinline__ bool bit_at(const unsigned long long *m, int i) { return (m[i >> 6] >> (i & 63)) & 1ull; }
 // any set bit in [lo, hi] (inclusive, lo >= 0)
 __device__ __forceinline__ bool any_bits(const unsigned long long *m, int lo, int hi) {
@@ -209,16 +253,37 @@ __device__ __forceinline__ float2 cfo_rot(float2 v, double f_ts, int i) {
     return make_float2(v.x * c - v.y * s, v.x * s + v.y * c);
 }
 
-struct FrSlots { unsigned long long v[10]; };   // per-SNR block accumulators
+// LDS image of one trial (dynamic shared memory, sized per launch by frame_lds_bytes)
+struct FrameLds {
+    float2 *r;                  // capture [cap_len]
+    float2 *fr;                 // down-sampled frame [fr_len(n_data)]
+    unsigned long long *cross;  // Packet_Detection threshold crossings, 1 bit per position
+    unsigned long long *acc;    // [n_snr][ACC_SLOTS] per-SNR block accumulators
+};
+constexpr int ACC_SLOTS = 12;   // 9 counter sums + word-length min / max (q20) + pad
+__host__ __device__ inline int cross_words(int cap_len) { return (cap_len - 47 + 63) / 64 + 1; }
+__host__ __device__ inline size_t frame_lds_bytes(int cap_len, int n_data, int n_snr) {
+    return (size_t)cap_len * 8 + (size_t)fr_len(n_data) * 8 + (size_t)cross_words(cap_len) * 8 +
+           (size_t)n_snr * ACC_SLOTS * 8;
+}
 
 __global__ __launch_bounds__(64) void frame_rx_kernel(FrameArgs a) {
-    __shared__ float2 r[CAP_MAX];
-    __shared__ float2 fr[FR_SAMPLES];
-    __shared__ unsigned long long cross[48];
-    __shared__ unsigned long long acc[OFDM_MAX_SNR][10];
-    const int lane = threadIdx.x;
-    for (int i = lane; i < a.n_snr * 10; i += 64) (&acc[0][0])[i] = 0ull;
+    extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
     const int L = a.cap_len, Lc = L - 47;       // Packet_Detection length (OFDM.c:663)
+    const int nfr = fr_len(a.n_data);
+    FrameLds s;
+    s.r = reinterpret_cast<float2 *>(smem);
+    s.fr = s.r + L;
+    s.cross = reinterpret_cast<unsigned long long *>(s.fr + nfr);
+    s.acc = s.cross + cross_words(L);
+    float2 *r = s.r, *fr = s.fr;
+    unsigned long long *cross = s.cross;
+    const int lane = threadIdx.x;
+    for (int i = lane; i < a.n_snr * ACC_SLOTS; i += 64) {
+        const int k = i % ACC_SLOTS;
+        s.acc[i] = k == 10 ? (unsigned long long)INT64_MAX : k == 11 ? (unsigned long long)INT64_MIN : 0ull;
+    }
+    const int chunk = (Lc + 63) / 64;           // detection positions per lane (< 300: one front each)
     const int64_t items = a.n_trials * a.n_snr;
     for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
         const int q = (int)(it % a.n_snr);
@@ -237,7 +302,7 @@ __global__ __launch_bounds__(64) void frame_rx_kernel(FrameArgs a) {
         } else {
             const int b0 = rx_start >> 2, b1 = (rx_start + L - 1) >> 2;
             // Gaussian k of the trial's stream goes to waveform sample k (as if Transmission_Over_Air
-            // had drawn all 9800); only the captured samples are ever evaluated
+            // had drawn the whole waveform); only the captured samples are ever evaluated
             for (int b = b0 + lane; b <= b1; b += 64) {
                 Gauss4 g;
                 if (a.noise == OFDM_NOISE_REAL) g = gauss4(t_lo, t_hi, (uint32_t)b, STREAM_NOISE | qs, a.k0, a.k1);
@@ -252,13 +317,39 @@ __global__ __launch_bounds__(64) void frame_rx_kernel(FrameArgs a) {
                 }
             }
         }
-        if (lane < 48) cross[lane] = 0ull;
+        for (int i = lane; i < cross_words(L); i += 64) cross[i] = 0ull;
         __syncthreads();
 
+        // ---- Word_Optimization_Analysis(Rx_filter_signal) (OFDM.c:38-73, 962-967): the full RRC
+        // matched filter of the capture, min / max over real and imaginary parts (opt-in) ----
+        if (a.word_stats) {
+            float mn = 1e9f, mx = -1e9f;
+            for (int k = lane; k < L + 20; k += 64) {
+                float2 v = make_float2(0.f, 0.f);
+#pragma unroll
+                for (int j = 0; j < 21; ++j) {
+                    const int m = k - j;
+                    if (m >= 0 && m < L) {
+                        v.x = fmaf(r[m].x, a.taps[j], v.x);
+                        v.y = fmaf(r[m].y, a.taps[j], v.y);
+                    }
+                }
+                mn = fminf(mn, fminf(v.x, v.y));
+                mx = fmaxf(mx, fmaxf(v.x, v.y));
+            }
+            mn = wave_min_f(mn);
+            mx = wave_max_f(mx);
+            if (lane == 0) {
+                unsigned long long *sl = s.acc + q * ACC_SLOTS;
+                sl[10] = (unsigned long long)min((long long)sl[10], (long long)__float2ll_rn(mn * (float)OFDM_EVM_Q_SCALE));
+                sl[11] = (unsigned long long)max((long long)sl[11], (long long)__float2ll_rn(mx * (float)OFDM_EVM_Q_SCALE));
+            }
+        }
+
         // ---- Packet_Detection (OFDM.c:659-683): M[n] = |sum r[n+k] r[n+k+16]|^2 / (sum |r[n+k+16]|^2)^2,
-        // k < 32, no conjugate, on the UNFILTERED capture; sliding sums over each lane's chunk ----
-        const int n0 = lane * CHUNK, n1 = min(n0 + CHUNK, Lc);
-        unsigned long long mask = 0ull;
+        // k < 32, no conjugate, on the UNFILTERED capture; sliding sums over each lane's chunk, the
+        // > 0.75 crossings (Packet_Selection's threshold, OFDM.c:687) kept as a bit mask ----
+        const int n0 = lane * chunk, n1 = min(n0 + chunk, Lc);
         if (n0 < n1) {
             float sx = 0.f, sy = 0.f, pw = 0.f;
             for (int k = 0; k < 32; ++k) {
@@ -267,10 +358,15 @@ __global__ __launch_bounds__(64) void frame_rx_kernel(FrameArgs a) {
                 sy += u.x * v.y + u.y * v.x;
                 pw += v.x * v.x + v.y * v.y;
             }
+            unsigned long long word = 0ull;
             for (int n = n0; n < n1; ++n) {
                 const float M = (sx * sx + sy * sy) / (pw * pw);
-                if (M > 0.75f) mask |= 1ull << (n - n0);          // Packet_Selection threshold (OFDM.c:687)
+                if (M > 0.75f) word |= 1ull << (n & 63);
                 if (a.dbg_corr && it == 0) a.dbg_corr[n] = M;
+                if ((n & 63) == 63 || n + 1 == n1) {
+                    if (word) atomicOr(&cross[n >> 6], word);
+                    word = 0ull;
+                }
                 if (n + 1 < n1) {
                     const float2 o0 = r[n], o1 = r[n + 16], i0 = r[n + 32], i1 = r[n + 48];
                     sx += (i0.x * i1.x - i0.y * i1.y) - (o0.x * o1.x - o0.y * o1.y);
@@ -278,19 +374,22 @@ __global__ __launch_bounds__(64) void frame_rx_kernel(FrameArgs a) {
                     pw += (i1.x * i1.x + i1.y * i1.y) - (o1.x * o1.x + o1.y * o1.y);
                 }
             }
-            atomicOr(&cross[n0 >> 6], mask << (n0 & 63));
-            if ((n0 & 63) + CHUNK > 64) atomicOr(&cross[(n0 >> 6) + 1], mask >> (64 - (n0 & 63)));
         }
         __syncthreads();
 
         // ---- Packet_Selection (OFDM.c:685-771): a crossing i is a front iff i - prev > 300 with
         // prev = previous crossing or -1, i.e. i >= 300 and no crossing in [i-300, i-1]; the first
         // front x with a later front and M[front+230] > 0.75 gives packet_idx = front + 11.  Fronts
-        // are > 300 apart, so a lane's 47-wide chunk holds at most one. ----
+        // are > 300 apart, so a lane's chunk (< 300 positions) holds at most one. ----
         int front = -1;
-        for (unsigned long long m = mask; m; m &= m - 1) {
-            const int i = n0 + __builtin_ctzll(m);
-            if (i >= 300 && !(i >= 1 && bit_at(cross, i - 1)) && !any_bits(cross, i - 300, i - 1)) { front = i; break; }
+        for (int wd = n0 >> 6; n0 < n1 && wd <= ((n1 - 1) >> 6) && front < 0; ++wd) {
+            unsigned long long m = cross[wd];
+            if (wd == (n0 >> 6)) m &= ~0ull << (n0 & 63);
+            if (wd == ((n1 - 1) >> 6) && ((n1 - 1) & 63) != 63) m &= (1ull << (((n1 - 1) & 63) + 1)) - 1ull;
+            for (; m; m &= m - 1) {
+                const int i = (wd << 6) + __builtin_ctzll(m);
+                if (i >= 300 && !any_bits(cross, i - 300, i - 1)) { front = i; break; }
+            }
         }
         const bool valid = front >= 0 && front + 230 < Lc && bit_at(cross, front + 230);
         const int maxf = wave_max_i(front);
@@ -300,7 +399,7 @@ __global__ __launch_bounds__(64) void frame_rx_kernel(FrameArgs a) {
 
         // ---- RRC matched filter at the down-sampled instants p + 2i (OFDM.c:965, 992-996) ----
         bool oob_l = false;
-        for (int i = lane; i < FR_SAMPLES; i += 64) {
+        for (int i = lane; i < nfr; i += 64) {
             const int n = p + 2 * i;
             float2 v = make_float2(0.f, 0.f);
             if (n >= L + 20) {
@@ -327,7 +426,7 @@ __global__ __launch_bounds__(64) void frame_rx_kernel(FrameArgs a) {
         px = wave_sum_f(px); py = wave_sum_f(py);
         double fc = (-1.0 / (2.0 * M_PI * 16.0 * TS)) * (double)atan2f(py, px);
         if (a.float_cfo) fc = (double)(float)fc;
-        for (int i = lane; i < FR_SAMPLES; i += 64) fr[i] = cfo_rot(fr[i], fc * TS, i);
+        for (int i = lane; i < nfr; i += 64) fr[i] = cfo_rot(fr[i], fc * TS, i);
         __syncthreads();
         // ---- Fine CFO (OFDM.c:806-828): 64-lag over the two long training symbols ----
         {
@@ -338,14 +437,17 @@ __global__ __launch_bounds__(64) void frame_rx_kernel(FrameArgs a) {
         double ff = (-1.0 / (2.0 * M_PI * 64.0 * TS)) * (double)atan2f(py, px);
         if (a.float_cfo) ff = (double)(float)ff;
         __syncthreads();
-        for (int i = lane; i < FR_SAMPLES; i += 64) fr[i] = cfo_rot(fr[i], ff * TS, i);
+        for (int i = lane; i < nfr; i += 64) fr[i] = cfo_rot(fr[i], ff * TS, i);
         __syncthreads();
-        if (a.dbg_frame && it == 0) for (int i = lane; i < FR_SAMPLES; i += 64) a.dbg_frame[i] = fr[i];
+        if (a.dbg_frame && it == 0) for (int i = lane; i < nfr; i += 64) a.dbg_frame[i] = fr[i];
 
-        // ---- LS estimate + CP strip + fft + ZF + slicer + demap (OFDM.c:830-1100); every quad
-        // computes the same 4 windows {LTF1, LTF2, D0, D1}, quad 0 reports ----
+        // ---- LS estimate + CP strip + fft + ZF + slicer + demap (OFDM.c:830-1100).  Quad k carries
+        // {LTF1, LTF2, D_2k, D_2k+1}: the estimate is formed inside each quad (two broadcasts) ----
         const int role = lane & 3;
-        const int w0 = role == 0 ? 192 : role == 1 ? 256 : (role == 2 ? 336 : 416);
+        const int dsym = 2 * (lane >> 2) + (role & 1);
+        const bool dlane = role >= 2 && dsym < a.n_data;
+        const int dsc = min(dsym, a.n_data - 1);
+        const int w0 = role == 0 ? 192 : role == 1 ? 256 : 336 + 80 * dsc;
         float2 x[64];
         static_for<0, 64>([&](auto nc) {
             constexpr int n = decltype(nc)::value;
@@ -353,64 +455,68 @@ __global__ __launch_bounds__(64) void frame_rx_kernel(FrameArgs a) {
             x[n] = (n & 1) ? make_float2(-v.x, -v.y) : v;        // fft() = DFT(x (-1)^n)
         });
         fft64<false>(x);
-        const uint32_t w[3] = {a.table[3 * (role & 1)], a.table[3 * (role & 1) + 1], a.table[3 * (role & 1) + 2]};
+        const uint32_t w[3] = {a.table[3 * dsc], a.table[3 * dsc + 1], a.table[3 * dsc + 2]};
         SymState st;
         sym_init(st);
-        const bool dump = a.dbg_eq && it == 0 && lane < 4 && role >= 2;
-        float2 *deq = dump ? a.dbg_eq + 48 * (role - 2) : nullptr;
+        const bool dump = a.dbg_eq && it == 0 && dlane;
+        float2 *deq = dump ? a.dbg_eq + 48 * dsym : nullptr;
         auto Hof = [&](float2 Y, auto binc) { return ls_equalise<decltype(binc)::value>(Y); };
         static_for<0, 4>([&](auto rc) { demap_sub<true, decltype(rc)::value, 2>(x, w, Hof, deq, st); });
-        const uint32_t be = st.be, ax = st.ax;
-        const float evm = finish_evm<2>(st);
-        const float e_other = dpp_f<0xB1>(evm);
-        const uint32_t be_other = dpp_u<0xB1>(be), ax_other = dpp_u<0xB1>(ax);
-        if (lane == 2) {
-            const float fe = evm + e_other;
-            const uint32_t ferr = be + be_other, fax = ax + ax_other;
-            unsigned long long *s = acc[q];
-            s[0] += ferr;
-            s[1] += ferr > 0u;
-            s[2] += fax;
-            s[3] += sync_fail;
-            s[4] += oob;
-            const float N = 96.0f;
-            s[5] += (unsigned long long)(int64_t)__float2ll_rn(fe * (float)OFDM_EVM_Q_SCALE);
+        const float fe = wave_sum_f(dlane ? finish_evm<2>(st) : 0.f);
+        const uint32_t ferr = wave_sum_u32(dlane ? st.be : 0u), fax = wave_sum_u32(dlane ? st.ax : 0u);
+        if (lane == 0) {
+            unsigned long long *sl = s.acc + q * ACC_SLOTS;
+            sl[0] += ferr;
+            sl[1] += ferr > 0u;
+            sl[2] += fax;
+            sl[3] += sync_fail;
+            sl[4] += oob;
+            const float N = 48.0f * (float)a.n_data;
+            sl[5] += (unsigned long long)(int64_t)__float2ll_rn(fe * (float)OFDM_EVM_Q_SCALE);
             const float db = fe > 0.f ? fmaxf(3.01029995663981195214f * __builtin_amdgcn_logf(fe / N), -400.f) : -400.f;
-            s[6] += (unsigned long long)(int64_t)__float2ll_rn(db * (float)OFDM_EVM_Q_SCALE);
+            sl[6] += (unsigned long long)(int64_t)__float2ll_rn(db * (float)OFDM_EVM_Q_SCALE);
             float dbp = -INFINITY;
             if (fax > 0u) {
                 dbp = 3.01029995663981195214f * __builtin_amdgcn_logf(2.0f * (float)fax / N);
-                s[7] += (unsigned long long)(int64_t)__float2ll_rn(dbp * (float)OFDM_EVM_Q_SCALE);
-                s[8] += 1ull;
+                sl[7] += (unsigned long long)(int64_t)__float2ll_rn(dbp * (float)OFDM_EVM_Q_SCALE);
+                sl[8] += 1ull;
             }
             if (a.pidx_out) a.pidx_out[(int64_t)q * a.n_trials + ti] = p;
             if (it == 0) {
-                if (a.dbg_res) { a.dbg_res[0] = db; a.dbg_res[1] = dbp; a.dbg_res[2] = (float)ferr / 192.0f; }
+                if (a.dbg_res) { a.dbg_res[0] = db; a.dbg_res[1] = dbp; a.dbg_res[2] = (float)ferr / (96.0f * a.n_data); }
                 if (a.dbg_ints) { a.dbg_ints[0] = p; a.dbg_ints[1] = sync_fail; a.dbg_ints[2] = oob; a.dbg_ints[3] = rx_start; }
             }
         }
-        if (it == 0 && a.dbg_bits && lane >= 2 && lane < 4) {
-            a.dbg_bits[3 * (lane - 2)] = st.d[0]; a.dbg_bits[3 * (lane - 2) + 1] = st.d[1]; a.dbg_bits[3 * (lane - 2) + 2] = st.d[2];
+        if (it == 0 && a.dbg_bits && dlane) {
+            a.dbg_bits[3 * dsym] = st.d[0]; a.dbg_bits[3 * dsym + 1] = st.d[1]; a.dbg_bits[3 * dsym + 2] = st.d[2];
         }
         __syncthreads();
     }
     __syncthreads();
     for (int i = lane; i < a.n_snr * 9; i += 64) {
         const int q = i / 9, k = i % 9;
-        const unsigned long long v = acc[q][k];
+        const unsigned long long v = s.acc[q * ACC_SLOTS + k];
         if (!v) continue;
         const int c = k == 0 ? OFDM_C_BIT_ERR : k == 1 ? OFDM_C_FRAME_ERR : k == 2 ? OFDM_C_EVM_POST_AXIS
                     : k == 3 ? OFDM_C_SYNC_FAIL : k == 4 ? OFDM_C_OOB : k == 5 ? OFDM_C_EVM_PRE_Q
                     : k == 6 ? OFDM_C_EVMDB_PRE_Q : k == 7 ? OFDM_C_EVMDB_POST_Q : OFDM_C_EVMDB_POST_FINITE;
         atomicAdd(&a.counters[q * OFDM_NCOUNTERS + c], v);
     }
+    if (a.word_stats) {
+        for (int q = lane; q < a.n_snr; q += 64) {
+            long long *c = reinterpret_cast<long long *>(a.counters + q * OFDM_NCOUNTERS);
+            atomicMin(&c[OFDM_C_WL_MIN_Q], (long long)s.acc[q * ACC_SLOTS + 10]);
+            atomicMax(&c[OFDM_C_WL_MAX_Q], (long long)s.acc[q * ACC_SLOTS + 11]);
+        }
+    }
     if (blockIdx.x == 0) {
         for (int q = lane; q < a.n_snr; q += 64) {
             unsigned long long *c = a.counters + q * OFDM_NCOUNTERS;
-            atomicAdd(&c[OFDM_C_FRAMES], (unsigned long long)a.n_trials);
-            atomicAdd(&c[OFDM_C_SYMBOLS], (unsigned long long)(2 * a.n_trials));
-            atomicAdd(&c[OFDM_C_BITS], (unsigned long long)(192 * a.n_trials));
-            atomicAdd(&c[OFDM_C_EVM_TERMS], (unsigned long long)(96 * a.n_trials));
+            const unsigned long long nt = (unsigned long long)a.n_trials, nd = (unsigned long long)a.n_data;
+            atomicAdd(&c[OFDM_C_FRAMES], nt);
+            atomicAdd(&c[OFDM_C_SYMBOLS], nd * nt);
+            atomicAdd(&c[OFDM_C_BITS], 96ull * nd * nt);
+            atomicAdd(&c[OFDM_C_EVM_TERMS], 48ull * nd * nt);
         }
     }
 }
@@ -451,14 +557,15 @@ static int ensure_wave(Ctx *c, int conv, int payload) {
     if (conv != OFDM_CONV_C && conv != OFDM_CONV_MATLAB) return set_error(OFDM_E_ARG, "bad conv %d", conv);
     if (payload != OFDM_PAYLOAD_MESSAGE && payload != OFDM_PAYLOAD_TESTER)
         return set_error(OFDM_E_ARG, "frame mode needs a fixed payload (MESSAGE or TESTER), got %d", payload);
-    const int key = conv * 4 + payload;
+    const int key = conv * 4 + payload;      // ofdm_set_message resets the key
     if (c->wave_key == key) return OFDM_OK;
-    int rc = c->ensure(&c->d_wave, &c->cap_wave, WAVE_LEN * sizeof(float2) + 64);
-    if (rc) return rc;
     WaveArgs a{};
+    a.n_data = payload_table(payload, c->message, a.table);
+    const int len = wave_len_for(a.n_data);
+    int rc = c->ensure(&c->d_wave, &c->cap_wave, (size_t)len * sizeof(float2) + 64);
+    if (rc) return rc;
     a.wave = (float2 *)c->d_wave;
-    a.power = (double *)((char *)c->d_wave + WAVE_LEN * sizeof(float2));
-    payload_table(payload, a.table);
+    a.power = (double *)((char *)c->d_wave + (size_t)len * sizeof(float2));
     rrc_taps(a.taps);
     a.stf_scale = (float)std::sqrt(13.0 / 6.0);
     if (conv == OFDM_CONV_C) hipLaunchKernelGGL(frame_wave_kernel<OFDM_CONV_C>, dim3(1), dim3(256), 0, c->stream, a);
@@ -467,36 +574,49 @@ static int ensure_wave(Ctx *c, int conv, int payload) {
     HIPOK(hipMemcpyAsync(&c->wave_power, a.power, sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIPOK(hipStreamSynchronize(c->stream));
     c->wave_key = key;
-    c->wave_len = WAVE_LEN;
+    c->wave_len = len;
+    c->wave_frames = a.n_data;
     return OFDM_OK;
 }
 
-static int check_opts(const ofdm_rx_opts *o) {
+// capture length: opts->cap_len, or the reference's int(0.307 * len) when 0 (OFDM.c:945)
+static int capture_len(const Ctx *c, const ofdm_rx_opts *o) { return o->cap_len ? o->cap_len : cap_len_for(c->wave_frames); }
+
+static int check_opts(const Ctx *c, const ofdm_rx_opts *o) {
     if (!o) return set_error(OFDM_E_ARG, "opts is NULL");
-    if (o->cap_len < 400 || o->cap_len > CAP_MAX) return set_error(OFDM_E_ARG, "cap_len must be in [400, %d]", CAP_MAX);
-    if (o->fixed_start > WAVE_LEN - o->cap_len) return set_error(OFDM_E_ARG, "fixed_start beyond the waveform");
+    const int L = capture_len(c, o);
+    if (L < 400 || L > CAP_ABS_MAX || L > c->wave_len)
+        return set_error(OFDM_E_ARG, "cap_len %d must be in [400, min(%d, waveform %d)]", L, CAP_ABS_MAX, c->wave_len);
+    if (o->fixed_start > c->wave_len - L) return set_error(OFDM_E_ARG, "fixed_start beyond the waveform");
     return OFDM_OK;
 }
 
 static void fill_frame_args(FrameArgs &a, Ctx *c, const ofdm_rx_opts *o, int noise, uint64_t seed, int payload) {
     a.wave = (const float2 *)c->d_wave;
-    a.cap_len = o->cap_len;
+    a.cap_len = capture_len(c, o);
     a.float_cfo = o->float_cfo;
     a.matlab = o->matlab_slicer;
     a.fixed_start = o->fixed_start;
     a.noise = noise;
-    a.wave_len = WAVE_LEN;
+    a.wave_len = c->wave_len;
     a.k0 = (uint32_t)seed;
     a.k1 = (uint32_t)(seed >> 32);
-    payload_table(payload, a.table);
+    a.n_data = payload_table(payload, c->message, a.table);
+    a.word_stats = o->word_stats ? 1 : 0;
     rrc_taps(a.taps);
 }
 
-static unsigned frame_grid(Ctx *c, int64_t items) {
+// bits needed for the largest magnitude, as OFDM.c:56-64
+static int32_t word_bits(double mn, double mx) {
+    const float max_abs = (float)std::fmax(std::fabs(mn), std::fabs(mx));
+    return max_abs < 1.0f ? 1 : (int32_t)std::ceil(std::log2((double)max_abs)) + 1;
+}
+
+static unsigned frame_grid(Ctx *c, int64_t items, size_t lds) {
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(&frame_rx_kernel), 64, 0) !=
-            hipSuccess || per_cu < 1)
-        per_cu = 4;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(&frame_rx_kernel), 64,
+                                                     lds) != hipSuccess || per_cu < 1)
+        per_cu = 2;
     const int64_t cap = (int64_t)per_cu * c->cus * 4;
     return (unsigned)std::max<int64_t>(1, std::min(items, cap));
 }
@@ -508,13 +628,13 @@ int ofdm_transmitter(ofdm_ctx *ctx, int conv, int payload, int float_taps, float
     Ctx *c = reinterpret_cast<Ctx *>(ctx);
     (void)float_taps;   // taps are fp32 on the GPU either way (OFDM.c:32 values)
     if (!c || !tx_out || !len_out) return set_error(OFDM_E_ARG, "bad transmitter arguments");
-    if (max_complex < WAVE_LEN) return set_error(OFDM_E_ARG, "tx_out needs %d complex samples", WAVE_LEN);
     HIPOK(hipSetDevice(c->device));
     int rc = ensure_wave(c, conv, payload);
     if (rc) return rc;
-    HIPOK(hipMemcpyAsync(tx_out, c->d_wave, WAVE_LEN * sizeof(float2), hipMemcpyDeviceToHost, c->stream));
+    if (max_complex < c->wave_len) return set_error(OFDM_E_ARG, "tx_out needs %d complex samples", c->wave_len);
+    HIPOK(hipMemcpyAsync(tx_out, c->d_wave, (size_t)c->wave_len * sizeof(float2), hipMemcpyDeviceToHost, c->stream));
     HIPOK(hipStreamSynchronize(c->stream));
-    *len_out = WAVE_LEN;
+    *len_out = c->wave_len;
     return OFDM_OK;
 }
 
@@ -544,15 +664,15 @@ int ofdm_receiver(ofdm_ctx *ctx, const float *capture, const ofdm_rx_opts *opts,
                   int32_t *ints4, int32_t *bits_out, float *eq_out) {
     Ctx *c = reinterpret_cast<Ctx *>(ctx);
     if (!c || !capture) return set_error(OFDM_E_ARG, "bad receiver arguments");
-    int rc = check_opts(opts);
-    if (rc) return rc;
     HIPOK(hipSetDevice(c->device));
-    if ((rc = ensure_wave(c, OFDM_CONV_C, payload))) return rc;
-    const int L = opts->cap_len;
+    int rc = ensure_wave(c, OFDM_CONV_C, payload);
+    if (rc) return rc;
+    if ((rc = check_opts(c, opts))) return rc;
+    const int L = capture_len(c, opts), nd = c->wave_frames;
     // scratch: capture | counters | res | ints | bits | eq
     const size_t off_cnt = ((size_t)L * sizeof(float2) + 255) & ~size_t(255);
     const size_t off_res = off_cnt + OFDM_NCOUNTERS * 8, off_int = off_res + 16, off_bits = off_int + 16;
-    const size_t off_eq = off_bits + 32, total = off_eq + 96 * sizeof(float2);
+    const size_t off_eq = off_bits + 4 * 3 * FR_MAX_DATA, total = off_eq + 48 * FR_MAX_DATA * sizeof(float2);
     if ((rc = c->ensure(&c->d_scratch2, &c->cap_scratch2, total))) return rc;
     char *base = (char *)c->d_scratch2;
     HIPOK(hipMemcpyAsync(base, capture, (size_t)L * sizeof(float2), hipMemcpyHostToDevice, c->stream));
@@ -569,24 +689,25 @@ int ofdm_receiver(ofdm_ctx *ctx, const float *capture, const ofdm_rx_opts *opts,
     a.dbg_ints = (int32_t *)(base + off_int);
     a.dbg_bits = (uint32_t *)(base + off_bits);
     a.dbg_eq = (float2 *)(base + off_eq);
+    const size_t lds = frame_lds_bytes(L, nd, 1);
     c->tic(Ctx::K_FRAME);
-    hipLaunchKernelGGL(frame_rx_kernel, dim3(1), dim3(64), 0, c->stream, a);
+    hipLaunchKernelGGL(frame_rx_kernel, dim3(1), dim3(64), lds, c->stream, a);
     c->toc();
     HIPOK(hipGetLastError());
     float res[4];
     int32_t ints[4];
-    uint32_t words[8];
-    float2 eq[96];
+    uint32_t words[3 * FR_MAX_DATA];
+    float2 eq[48 * FR_MAX_DATA];
     HIPOK(hipMemcpyAsync(res, base + off_res, 16, hipMemcpyDeviceToHost, c->stream));
     HIPOK(hipMemcpyAsync(ints, base + off_int, 16, hipMemcpyDeviceToHost, c->stream));
-    HIPOK(hipMemcpyAsync(words, base + off_bits, 32, hipMemcpyDeviceToHost, c->stream));
+    HIPOK(hipMemcpyAsync(words, base + off_bits, sizeof(words), hipMemcpyDeviceToHost, c->stream));
     HIPOK(hipMemcpyAsync(eq, base + off_eq, sizeof(eq), hipMemcpyDeviceToHost, c->stream));
     HIPOK(hipStreamSynchronize(c->stream));
     if (res3) { res3[0] = res[0]; res3[1] = res[1]; res3[2] = res[2]; }
-    if (ints4) { ints4[0] = ints[0]; ints4[1] = ints[1]; ints4[2] = ints[2]; ints4[3] = 0; }
+    if (ints4) { ints4[0] = ints[0]; ints4[1] = ints[1]; ints4[2] = ints[2]; ints4[3] = nd; }
     if (bits_out)
-        for (int b = 0; b < 192; ++b) bits_out[b] = (int32_t)((words[b / 32] >> (31 - (b & 31))) & 1u);
-    if (eq_out) std::memcpy(eq_out, eq, sizeof(eq));
+        for (int b = 0; b < 96 * nd; ++b) bits_out[b] = (int32_t)((words[b / 32] >> (31 - (b & 31))) & 1u);
+    if (eq_out) std::memcpy(eq_out, eq, (size_t)48 * nd * sizeof(float2));
     return OFDM_OK;
 }
 
@@ -596,17 +717,24 @@ int ofdm_frame_sweep(ofdm_ctx *ctx, const ofdm_cfg *cfg, const ofdm_rx_opts *opt
     if (!c) return set_error(OFDM_E_ARG, "ctx is NULL");
     int rc = check_cfg(cfg);
     if (rc) return rc;
-    if ((rc = check_opts(opts))) return rc;
+    if (!opts) return set_error(OFDM_E_ARG, "opts is NULL");
     if (n_snr < 0 || (n_snr && (!snr_db || !counters)) || n_trials < 0) return set_error(OFDM_E_ARG, "bad sweep args");
     if (cfg->channel != OFDM_CHAN_AWGN) return set_error(OFDM_E_ARG, "frame mode models the AWGN channel only");
     if (cfg->noise == OFDM_NOISE_COMPLEX) return set_error(OFDM_E_ARG, "frame mode noise is real (OFDM.c:651) or none");
     if (n_snr == 0) return OFDM_OK;
     HIPOK(hipSetDevice(c->device));
     if ((rc = ensure_wave(c, cfg->conv, cfg->payload))) return rc;
+    if ((rc = check_opts(c, opts))) return rc;
     const size_t cbytes = (size_t)n_snr * OFDM_NCOUNTERS * 8;
     const size_t pbytes = packet_idx ? (size_t)n_snr * n_trials * 4 : 0;
     if ((rc = c->ensure(&c->d_cnt, &c->cap_cnt, cbytes + pbytes + 256))) return rc;
-    HIPOK(hipMemsetAsync(c->d_cnt, 0, cbytes, c->stream));
+    std::vector<int64_t> init((size_t)n_snr * OFDM_NCOUNTERS, 0);
+    if (opts->word_stats)
+        for (int q = 0; q < n_snr; ++q) {
+            init[(size_t)q * OFDM_NCOUNTERS + OFDM_C_WL_MIN_Q] = INT64_MAX;
+            init[(size_t)q * OFDM_NCOUNTERS + OFDM_C_WL_MAX_Q] = INT64_MIN;
+        }
+    HIPOK(hipMemcpyAsync(c->d_cnt, init.data(), cbytes, hipMemcpyHostToDevice, c->stream));
     int32_t *dp = packet_idx ? (int32_t *)((char *)c->d_cnt + ((cbytes + 255) & ~size_t(255))) : nullptr;
     for (int q0 = 0; q0 < n_snr; q0 += OFDM_MAX_SNR) {
         FrameArgs a{};
@@ -620,14 +748,43 @@ int ofdm_frame_sweep(ofdm_ctx *ctx, const ofdm_cfg *cfg, const ofdm_rx_opts *opt
         for (int q = 0; q < a.n_snr; ++q)   // sigma^2 = P / 10^(snr/10) (OFDM.c:645-647)
             a.sigma[q] = (float)std::sqrt(c->wave_power / std::pow(10.0, snr_db[q0 + q] / 10.0));
         if (n_trials == 0) continue;
+        const size_t lds = frame_lds_bytes(a.cap_len, a.n_data, a.n_snr);
         c->tic(Ctx::K_FRAME);
-        hipLaunchKernelGGL(frame_rx_kernel, dim3(frame_grid(c, n_trials * a.n_snr)), dim3(64), 0, c->stream, a);
+        hipLaunchKernelGGL(frame_rx_kernel, dim3(frame_grid(c, n_trials * a.n_snr, lds)), dim3(64), lds, c->stream, a);
         c->toc();
         HIPOK(hipGetLastError());
     }
     HIPOK(hipMemcpyAsync(counters, c->d_cnt, cbytes, hipMemcpyDeviceToHost, c->stream));
     if (dp) HIPOK(hipMemcpyAsync(packet_idx, dp, pbytes, hipMemcpyDeviceToHost, c->stream));
     HIPOK(hipStreamSynchronize(c->stream));
+    if (opts->word_stats && n_trials > 0)
+        for (int q = 0; q < n_snr; ++q) {
+            int64_t *row = counters + (size_t)q * OFDM_NCOUNTERS;
+            row[OFDM_C_WL_BITS] = word_bits(row[OFDM_C_WL_MIN_Q] / OFDM_EVM_Q_SCALE, row[OFDM_C_WL_MAX_Q] / OFDM_EVM_Q_SCALE);
+        }
+    return OFDM_OK;
+}
+
+int ofdm_word_length_report(ofdm_ctx *ctx, const float *capture, int32_t cap_len, float *out3, int32_t *bits) {
+    Ctx *c = reinterpret_cast<Ctx *>(ctx);
+    if (!c || !capture || cap_len <= 0 || cap_len > (1 << 24)) return set_error(OFDM_E_ARG, "bad word-length arguments");
+    HIPOK(hipSetDevice(c->device));
+    const size_t bytes = (size_t)cap_len * sizeof(float2);
+    int rc = c->ensure(&c->d_scratch2, &c->cap_scratch2, bytes + 64);
+    if (rc) return rc;
+    float2 *dx = (float2 *)c->d_scratch2;
+    float *dout = (float *)((char *)c->d_scratch2 + bytes);
+    HIPOK(hipMemcpyAsync(dx, capture, bytes, hipMemcpyHostToDevice, c->stream));
+    FrameArgs a{};
+    rrc_taps(a.taps);
+    hipLaunchKernelGGL(word_length_kernel, dim3(1), dim3(256), 0, c->stream, (const float2 *)dx, (int)cap_len, a, dout);
+    HIPOK(hipGetLastError());
+    float mm[2];
+    HIPOK(hipMemcpyAsync(mm, dout, sizeof(mm), hipMemcpyDeviceToHost, c->stream));
+    HIPOK(hipStreamSynchronize(c->stream));
+    const float max_abs = std::fmax(std::fabs(mm[0]), std::fabs(mm[1]));
+    if (out3) { out3[0] = mm[0]; out3[1] = mm[1]; out3[2] = max_abs; }
+    if (bits) *bits = word_bits(mm[0], mm[1]);
     return OFDM_OK;
 }
 

@@ -32,7 +32,8 @@ struct TxArgs {
     int64_t pitch;
     uint32_t k0, k1;
     int32_t payload;
-    uint32_t table[6];                 // MESSAGE / TESTER payload words (2 symbols x 3 words)
+    int32_t table_frames;              // MESSAGE / TESTER: symbols in the payload table
+    uint32_t table[24];                // MESSAGE / TESTER payload words (3 per symbol; symbol s uses s % frames)
 };
 
 struct RxArgs {

@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256, 3) void tx_symbols_kernel(TxArgs a) {
         const uint4 o = philox10((uint32_t)s, (uint32_t)(s >> 32), 0u, STREAM_BITS, a.k0, a.k1);
         w[0] = o.x; w[1] = o.y; w[2] = o.z;
     } else {
-        const int r = (int)(s & 1);
+        const int r = (int)(s % (uint64_t)a.table_frames);
         w[0] = a.table[3 * r]; w[1] = a.table[3 * r + 1]; w[2] = a.table[3 * r + 2];
     }
     float2 X[64];

@@ -16,6 +16,7 @@ import numpy as np
 
 from . import abi
 from .abi import Cfg, RxOpts, check, load_library, make_cfg, make_rx_opts
+from .fileio import decode_message
 
 
 def _torch():
@@ -138,8 +139,20 @@ class Engine:
         return out
 
     # ---- frame mode (the reference's own trial) -----------------------------------------
+    def set_message(self, message: str | bytes) -> int:
+        """MESSAGE payload text (OFDM.c:20); returns the data symbols per frame, ceil(8 len / 96)."""
+        b = message.encode("latin-1") if isinstance(message, str) else bytes(message)
+        n = C.c_int32()
+        check(self.lib, self.lib.ofdm_set_message(self.ctx, b, len(b), C.byref(n)), "set_message")
+        return n.value
+
+    def payload_frames(self, payload: str = "message") -> int:
+        n = C.c_int32()
+        check(self.lib, self.lib.ofdm_payload_frames(self.ctx, abi.PAYLOAD[payload], C.byref(n)), "payload_frames")
+        return n.value
+
     def transmitter(self, conv: str = "c", payload: str = "message", float_taps: bool = True) -> np.ndarray:
-        cap = 20000
+        cap = abi.wave_len(8)
         buf = np.zeros(2 * cap, np.float32)
         n = C.c_int32()
         check(self.lib, self.lib.ofdm_transmitter(self.ctx, abi.CONV[conv], abi.PAYLOAD[payload], int(float_taps),
@@ -156,25 +169,40 @@ class Engine:
         return out
 
     def receiver(self, capture: np.ndarray, mode: str = "c", payload: str = "message"):
+        """Receiver() on one capture (OFDM.c:941-1182): metrics, packet_idx, bits, equalised
+        subcarriers and the decoded text (Message_Generator, OFDM.c:921-939)."""
         opts = make_rx_opts(mode)
-        cap = np.ascontiguousarray(capture[:opts.cap_len], np.complex64)
-        if len(cap) != opts.cap_len:
-            raise ValueError(f"capture must hold {opts.cap_len} samples")
+        nd = self.payload_frames(payload)
+        L = opts.cap_len or abi.capture_len(nd)
+        cap = np.ascontiguousarray(capture[:L], np.complex64)
+        if len(cap) != L:
+            raise ValueError(f"capture must hold {L} samples")
         res = np.zeros(3, np.float32); ints = np.zeros(4, np.int32)
-        bits = np.zeros(192, np.int32); eq = np.zeros(2 * 96, np.float32)
+        bits = np.zeros(96 * nd, np.int32); eq = np.zeros(2 * 48 * nd, np.float32)
         check(self.lib, self.lib.ofdm_receiver(self.ctx, cap.ctypes.data_as(C.c_void_p), C.byref(opts),
                                                abi.PAYLOAD[payload], res.ctypes.data_as(C.c_void_p),
                                                ints.ctypes.data_as(C.c_void_p), bits.ctypes.data_as(C.c_void_p),
                                                eq.ctypes.data_as(C.c_void_p)), "receiver")
-        return dict(res=res, packet_idx=int(ints[0]), sync_fail=int(ints[1]), oob=int(ints[2]), bits=bits,
-                    eq=eq.view(np.complex64).copy())
+        return dict(res=res, packet_idx=int(ints[0]), sync_fail=int(ints[1]), oob=int(ints[2]), frames=nd,
+                    bits=bits, eq=eq.view(np.complex64).copy(), message=decode_message(bits))
+
+    def word_length_report(self, capture: np.ndarray) -> dict:
+        """Word_Optimization_Analysis (OFDM.c:38-73) of the capture's RRC matched-filter output."""
+        cap = np.ascontiguousarray(capture, np.complex64)
+        out = np.zeros(3, np.float32)
+        bits = C.c_int32()
+        check(self.lib, self.lib.ofdm_word_length_report(self.ctx, cap.ctypes.data_as(C.c_void_p), len(cap),
+                                                         out.ctypes.data_as(C.c_void_p), C.byref(bits)),
+              "word_length_report")
+        return dict(min=float(out[0]), max=float(out[1]), max_abs=float(out[2]), bits=bits.value)
 
     def frame_sweep(self, cfg: Cfg, snr_db, n_trials: int, first_trial: int = 0, mode: str = "c",
-                    fixed_start: int = -1, want_packet_idx: bool = False):
+                    fixed_start: int = -1, want_packet_idx: bool = False, word_stats: bool = False):
         snr = np.ascontiguousarray(snr_db, np.float64)
         out = np.zeros((len(snr), abi.NCOUNTERS), np.int64)
         pidx = np.zeros((len(snr), n_trials), np.int32) if want_packet_idx else None
         opts = make_rx_opts(mode, fixed_start)
+        opts.word_stats = int(word_stats)
         check(self.lib, self.lib.ofdm_frame_sweep(self.ctx, C.byref(cfg), C.byref(opts), snr.ctypes.data_as(C.c_void_p),
                                                   len(snr), first_trial, n_trials, out.ctypes.data_as(C.c_void_p),
                                                   None if pidx is None else pidx.ctypes.data_as(C.c_void_p)),

@@ -63,3 +63,10 @@ def read_float_array_file(fname: str | os.PathLike) -> np.ndarray:
         else:
             out.append(float(w))
     return np.array(out)
+
+
+def decode_message(bits) -> str:
+    """Message_Generator / Binary_To_Decimal (OFDM.c:910-939): 8 bits MSB first per character."""
+    b = np.asarray(bits, dtype=np.int64).reshape(-1, 8)
+    codes = (b * (1 << np.arange(7, -1, -1))).sum(axis=1)
+    return bytes(int(c) & 0xFF for c in codes).decode("latin-1")

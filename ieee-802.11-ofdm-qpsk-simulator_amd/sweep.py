@@ -30,8 +30,10 @@ REF_SNR = np.arange(6.0, 41.0, 1.0)        # OFDM.c:18, 1197
 
 def run_sweep(engine: Engine, snr_db, trials: int, mode: str = "frame", seed: int = 0x80211A,
               payload: str | None = None, est: str = "ls", noise: str = "real", channel: str = "awgn",
-              conv: str = "c", rank: int = 0, world: int = 1) -> SweepResult:
+              conv: str = "c", rank: int = 0, world: int = 1, message: str | None = None) -> SweepResult:
     snr = np.asarray(snr_db, np.float64)
+    if message is not None:
+        engine.set_message(message)             # OFDM.c:20 `message`, framed by Data_Generator
     start, end = dist.shard_range(trials, rank, world)
     if mode == "frame":
         cfg = abi.make_cfg(seed=seed, conv=conv, payload=payload or "message", noise=noise)
@@ -79,11 +81,35 @@ def main(argv=None):
     ap.add_argument("--channel", choices=["awgn", "rayleigh4"], default="awgn")
     ap.add_argument("--conv", choices=["c", "matlab"], default="c")
     ap.add_argument("--payload", choices=["random", "message", "tester"])
+    ap.add_argument("--message", help="MESSAGE payload text (default: OFDM.c:20), up to 96 characters")
+    ap.add_argument("--print-messages", action="store_true",
+                    help="as OFDM.c:1167-1182: receive one capture per SNR point and print the decoded text")
     a = ap.parse_args(argv)
-    res = reference_main(a.out, a.trials, a.mode, np.array(a.snr) if a.snr else REF_SNR, a.seed, est=a.est,
-                         noise=a.noise, channel=a.channel, conv=a.conv, payload=a.payload)
+    snr = np.array(a.snr) if a.snr else REF_SNR
+    res = reference_main(a.out, a.trials, a.mode, snr, a.seed, est=a.est, noise=a.noise, channel=a.channel,
+                         conv=a.conv, payload=a.payload, message=a.message)
     for s, b, e in zip(res.snr_db, res.ber, res.evm_pre_db):
         print(f"SNR = {s:5.1f} dB   BER = {b:.3e}   EVM = {e:7.2f} dB", file=sys.stderr)
+    if a.print_messages:
+        for line in received_messages(snr, a.message, a.seed):
+            print(line)
+
+
+def received_messages(snr_db, message: str | None = None, seed: int = 0x80211A, device: int = 0):
+    """One reference trial per SNR point -- Transmission_Over_Air + capture + Receiver (OFDM.c:1202-1211)
+    -- yielding the console text the reference prints (OFDM.c:1177-1181)."""
+    with Engine(device) as eng:
+        if message is not None:
+            eng.set_message(message)
+        nd = eng.payload_frames("message")
+        w = eng.transmitter("c", "message")
+        L = abi.capture_len(nd)
+        rng = np.random.default_rng(seed)
+        for i, s in enumerate(np.asarray(snr_db, np.float64)):
+            ota = eng.transmission_over_air(w, float(s), seed=seed, trial=0, snr_index=i)
+            rs = int(rng.integers(0, len(w) - L))               # rand() % (len - cap) (OFDM.c:949)
+            o = eng.receiver(ota[rs:rs + L], "c", "message")
+            yield f"SNR = {s:.0f} dB\nReceived Message: \n{o['message']}"
 
 
 if __name__ == "__main__":

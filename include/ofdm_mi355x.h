@@ -60,6 +60,11 @@ extern "C" {
 #define OFDM_C_EVMDB_POST_Q 10     /* sum over frames with finite post-slicer EVM_dB, 2^-20 */
 #define OFDM_C_EVMDB_POST_FINITE 11
 #define OFDM_C_OOB 12              /* frame mode: down-sampler ran past the capture (ref reads garbage) */
+/* frame mode with ofdm_rx_opts.word_stats = 1: Word_Optimization_Analysis (OFDM.c:38-73) of every
+ * trial's RRC-filtered capture, aggregated per SNR point.  NOT sums: extremes over trials. */
+#define OFDM_C_WL_MIN_Q 13         /* min over trials of min(Re, Im), fixed point 2^-20 */
+#define OFDM_C_WL_MAX_Q 14         /* max over trials of max(Re, Im), fixed point 2^-20 */
+#define OFDM_C_WL_BITS 15          /* integer bits for max(|min|, |max|): 1 if < 1, else ceil(log2) + 1 */
 #define OFDM_EVM_Q_SCALE 1048576.0 /* 2^20 */
 
 typedef struct {
@@ -75,12 +80,14 @@ typedef struct {
 } ofdm_cfg;
 
 typedef struct {
-    int32_t cap_len;        /* capture length: 3008 = floor(0.307*9800) (OFDM.c:945) or 3000 (Tester.m:151) */
+    int32_t cap_len;        /* capture length: 0 = int(0.307 x waveform length) (OFDM.c:945; 3008 for the
+                               reference message) or e.g. 3000 (Tester.m:151) */
     int32_t float_cfo;      /* 1: CFO estimates rounded to float as OFDM.c:798,821 */
     int32_t matlab_slicer;  /* 1: MATLAB zero handling in slicer/demod (Tester.m:338-411) */
     int32_t float_taps;     /* 1: fp32 RRC taps (OFDM.c:32) -- 0: double rcosdesign taps */
     int32_t fixed_start;    /* >=0: capture offset for every trial (Tester.m:152); -1: Philox draw (OFDM.c:949) */
-    int32_t reserved[3];
+    int32_t word_stats;     /* 1: word-length analysis per trial into OFDM_C_WL_* (frame sweeps) */
+    int32_t reserved[2];
 } ofdm_rx_opts;
 
 typedef struct ofdm_ctx ofdm_ctx;
@@ -133,20 +140,35 @@ int ofdm_symbol_sweep(ofdm_ctx *ctx, const ofdm_cfg *cfg, const double *snr_db, 
                       uint64_t first_frame, int64_t n_frames, int64_t chunk_frames,
                       int64_t *counters);
 
+/* ---- payload text (SURVEY §8(f) message mode) ----
+ * MESSAGE payload = `msg` (default "Hey! I am Vivaswan", OFDM.c:20), MSB-first bytes padded with ' '
+ * to ceil(8 len / 96) data symbols per frame (Data_Generator, OFDM.c:435-465); 1 <= len <= 96 (frame
+ * mode carries at most 8 data symbols).  Symbol mode uses message symbol s mod frames for data
+ * symbol s.  `frames` (optional) receives the data symbols per frame. */
+int ofdm_set_message(ofdm_ctx *ctx, const char *msg, int32_t len, int32_t *frames);
+/* data symbols per frame of a fixed payload: MESSAGE (current message) or TESTER (2) */
+int ofdm_payload_frames(ofdm_ctx *ctx, int payload, int32_t *frames);
+
 /* ---- frame mode: the reference's own trial (preambles, RRC, packet sync, CFO), SURVEY §8 F1-F7 ----
  * "Transmitter()" (OFDM.c:467-618): writes the repeated RRC-filtered frame waveform (host,
- * interleaved, capacity max_complex) and its length; payload MESSAGE or TESTER. */
+ * interleaved, capacity max_complex) and its length 10 (2 (320 + 80 D) + 20) for D data symbols
+ * (9800 for the reference message); payload MESSAGE or TESTER. */
 int ofdm_transmitter(ofdm_ctx *ctx, int conv, int payload, int float_taps, float *tx_out,
                      int32_t max_complex, int32_t *len_out);
 /* "Transmission_Over_Air" (OFDM.c:635-655): real-only AWGN with var mean|tx|^2/10^(snr/10), Philox
  * stream (seed, trial, snr_index); host buffers of len complex samples. */
 int ofdm_transmission_over_air(ofdm_ctx *ctx, const float *tx, float *ota, int32_t len, double snr_db,
                                uint64_t seed, uint64_t trial, int32_t snr_index);
-/* "Receiver" (OFDM.c:941-1165) on one host capture already offset (cap_len samples): returns
- * res3 = {EVM_dB, EVM_AGC_dB, BER}, ints4 = {packet_idx, sync_fail, oob, reserved}, and optionally
- * the demodulated bits (int32 [2*96]) and equalised subcarriers (float2 [2*48]). */
+/* "Receiver" (OFDM.c:941-1165) on one host capture already offset (cap_len samples; cap_len 0 =
+ * int(0.307 x waveform length), OFDM.c:945): returns res3 = {EVM_dB, EVM_AGC_dB, BER},
+ * ints4 = {packet_idx, sync_fail, oob, D}, and optionally the demodulated bits (int32 [D*96]) and
+ * equalised subcarriers (float2 [D*48]), D = ofdm_payload_frames(payload). */
 int ofdm_receiver(ofdm_ctx *ctx, const float *capture, const ofdm_rx_opts *opts, int payload,
                   float *res3, int32_t *ints4, int32_t *bits_out, float *eq_out);
+/* "Word_Optimization_Analysis(Rx_filter_signal, len)" (OFDM.c:38-73, called at :967): the RRC
+ * matched filter of a capture (full convolution, cap_len + 20 outputs, OFDM.c:962-965), then
+ * out3 = {min, max, max |.|} over real and imaginary parts and the integer bits it needs. */
+int ofdm_word_length_report(ofdm_ctx *ctx, const float *capture, int32_t cap_len, float *out3, int32_t *bits);
 /* Batched frame-mode sweep: n_trials reference trials per SNR point (capture offset + noise from
  * Philox); host counters [n_snr][OFDM_NCOUNTERS]; optional per-trial packet_idx
  * [n_snr][n_trials]. */

@@ -401,7 +401,24 @@ void orc_receiver_frame(const double *capture, const orc_rx_opts *o, const int *
 }
 
 /* ===================================================================== Monte-Carlo twins */
-static const unsigned char REF_MESSAGE[] = "Hey! I am Vivaswan";   /* OFDM.c:20 */
+/* MESSAGE payload text: OFDM.c:20 by default, orc_set_message for message-mode tests */
+static unsigned char g_msg[97] = "Hey! I am Vivaswan";
+static int g_msg_len = 18;
+
+int orc_set_message(const unsigned char *msg, int len)
+{
+    if (len < 1 || len > 96) return -1;
+    memcpy(g_msg, msg, (size_t)len);
+    g_msg_len = len;
+    return (8 * len + 95) / 96;
+}
+
+/* bits of the fixed payloads: returns the data symbols per frame */
+static int fixed_payload_bits(int payload, int *bits)
+{
+    if (payload == ORC_PAYLOAD_TESTER) { orc_tester_bits(bits); return 2; }
+    return orc_message_bits(g_msg, g_msg_len, bits);
+}
 
 static void payload_bits(const orc_cfg *cfg, uint64_t s, int *bits96)
 {
@@ -412,10 +429,9 @@ static void payload_bits(const orc_cfg *cfg, uint64_t s, int *bits96)
         orc_philox4x32_10(ctr, key, o);
         for (int b = 0; b < 96; ++b) bits96[b] = (o[b >> 5] >> (31 - (b & 31))) & 1;
     } else {
-        int all[192];
-        if (cfg->payload == ORC_PAYLOAD_MESSAGE) orc_message_bits(REF_MESSAGE, 18, all);
-        else orc_tester_bits(all);
-        memcpy(bits96, all + 96 * (s & 1), sizeof(int) * 96);
+        int all[96 * 8];
+        const int nf = fixed_payload_bits(cfg->payload, all);   /* data symbol s carries message symbol s mod nf */
+        memcpy(bits96, all + 96 * (int)(s % (uint64_t)nf), sizeof(int) * 96);
     }
 }
 
@@ -546,10 +562,8 @@ void orc_symbol_sweep(const orc_cfg *cfg, const double *snr_db, int n_snr,
 void orc_frame_sweep(const orc_cfg *cfg, const orc_rx_opts *o, const double *snr_db, int n_snr,
                      uint64_t first_trial, uint64_t n_trials, int64_t *counters, int *dump_pidx)
 {
-    int bits[192];
-    if (cfg->payload == ORC_PAYLOAD_TESTER) orc_tester_bits(bits);
-    else orc_message_bits(REF_MESSAGE, 18, bits);
-    const int nf = 2, reps = 10;
+    int bits[96 * 8];
+    const int nf = fixed_payload_bits(cfg->payload, bits), reps = 10;
     const int len = (2 * (320 + 80 * nf) + 20) * reps;
     double *wf = malloc(sizeof(double) * 2 * len);
     orc_frame_waveform(bits, nf, cfg->conv, o->float_taps, reps, wf);
@@ -579,7 +593,7 @@ void orc_frame_sweep(const orc_cfg *cfg, const orc_rx_opts *o, const double *snr
                 cap[2 * n + 1] = wf[2 * k + 1];
             }
             orc_rx_info info;
-            int rb[192];
+            int rb[96 * 8];
             orc_receiver_frame(cap, o, bits, nf, NULL, NULL, NULL, NULL, NULL, NULL, NULL, rb, &info);
             if (dump_pidx) dump_pidx[(size_t)q * n_trials + ti] = info.packet_idx;
             int ferr = 0;
@@ -615,4 +629,25 @@ double orc_time_symbol_sweep(const orc_cfg *cfg, const double *snr_db, int n_snr
     orc_symbol_sweep(cfg, snr_db, n_snr, 0, n_frames, counters, NULL, NULL);
     clock_gettime(CLOCK_MONOTONIC, &t1);
     return (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
+}
+
+/* Word_Optimization_Analysis (OFDM.c:38-73) of Convolution(capture, RRC) (OFDM.c:342-364, 962-967):
+ * min / max over the real and imaginary parts of all n + 20 outputs, max |.|, integer bits. */
+int orc_word_length(const double *capture, int n, int float_taps, double *min_max_abs3)
+{
+    double h[21];
+    orc_rrc_taps(float_taps, h);
+    const cplx *x = (const cplx *)capture;
+    double mn = 1e9, mx = -1e9;
+    for (int k = 0; k < n + 20; ++k) {
+        cplx acc = 0;
+        for (int j = 0; j < 21; ++j) if (k - j >= 0 && k - j < n) acc += x[k - j] * h[j];
+        if (creal(acc) < mn) mn = creal(acc);
+        if (creal(acc) > mx) mx = creal(acc);
+        if (cimag(acc) < mn) mn = cimag(acc);
+        if (cimag(acc) > mx) mx = cimag(acc);
+    }
+    const double ma = fmax(fabs(mn), fabs(mx));
+    min_max_abs3[0] = mn; min_max_abs3[1] = mx; min_max_abs3[2] = ma;
+    return ma < 1.0 ? 1 : (int)ceil(log2(ma)) + 1;
 }

@@ -59,12 +59,14 @@ void orc_ifft64(const double *in, double *out, int conv);   /* ifft() (C) / ifft
 
 /* ---- transmitter primitives ---- */
 int  orc_message_bits(const unsigned char *msg, int len, int *bits_out);  /* returns frames */
+int  orc_set_message(const unsigned char *msg, int len);   /* MESSAGE payload text; returns frames */
 void orc_tester_bits(int *bits192);                                       /* Tester.m:50-51 */
 void orc_qpsk_map(const int *bits96, double *sym48);                      /* OFDM.c:415-433 */
 void orc_subcarrier_map(const double *sym48, double *X64);                /* OFDM.c:523-548 */
 void orc_preambles(int conv, double *stf160, double *ltf160, double *lf64);
 void orc_data_symbol(const int *bits96, int conv, double *time80);        /* map+ifft+CP */
 void orc_rrc_taps(int float_rounded, double *h21);                        /* OFDM.c:32 */
+int  orc_word_length(const double *capture, int n, int float_taps, double *min_max_abs3);  /* OFDM.c:38-73 */
 /* whole reference waveform: preambles + nf data symbols, 2x zero-stuff, RRC, x reps */
 int  orc_frame_waveform(const int *bits, int nf, int conv, int float_taps, int reps, double *out);
 

@@ -83,6 +83,26 @@ class Oracle:
             [C.c_void_p] * 8 + [C.POINTER(_RxInfo)]
         L.orc_frame_waveform.restype = C.c_int
         L.orc_message_bits.restype = C.c_int
+        L.orc_set_message.restype = C.c_int
+        L.orc_word_length.restype = C.c_int
+        L.orc_word_length.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
+        L.orc_set_message.argtypes = [C.c_char_p, C.c_int]
+        self._frames = 2
+
+    def word_length(self, capture: np.ndarray, float_taps: bool = True):
+        """Word_Optimization_Analysis of the RRC-filtered capture -> (min, max, max_abs, bits)."""
+        out = np.zeros(3)
+        cap = c2i(np.asarray(capture))
+        bits = self.lib.orc_word_length(_p(cap), len(capture), int(float_taps), _p(out))
+        return out[0], out[1], out[2], bits
+
+    def set_message(self, msg: bytes) -> int:
+        """MESSAGE payload text used by the sweeps (default OFDM.c:20); returns data symbols per frame."""
+        n = self.lib.orc_set_message(bytes(msg), len(msg))
+        if n < 0:
+            raise ValueError("message length must be 1..96")
+        self._frames = n
+        return n
 
     # ---- small helpers -------------------------------------------------------
     @staticmethod
@@ -92,9 +112,9 @@ class Oracle:
                     kappa, p_ref)
 
     @staticmethod
-    def rx_opts(mode="c") -> _RxOpts:
-        if mode == "c":
-            return _RxOpts(3008, 1, 0, 1)
+    def rx_opts(mode="c", frames: int = 2) -> _RxOpts:
+        if mode == "c":   # int(0.307 x waveform length) (OFDM.c:945): 3008 for 2 data symbols
+            return _RxOpts(int(10 * (2 * (320 + 80 * frames) + 20) * 0.307), 1, 0, 1)
         return _RxOpts(3000, 0, 1, 0)     # MATLAB Tester (Tester.m:151-152)
 
     def philox(self, ctr, key) -> np.ndarray:
@@ -153,10 +173,10 @@ class Oracle:
         return i2c(o)
 
     def receiver_frame(self, capture: np.ndarray, truth_bits, mode="c", dumps=False):
-        opts = self.rx_opts(mode)
-        cap = c2i(capture[:opts.cap_len])
         tb = np.ascontiguousarray(truth_bits, np.int32)
         nf = len(tb) // 96
+        opts = self.rx_opts(mode, nf)
+        cap = c2i(capture[:opts.cap_len])
         fsz = 320 + 80 * nf
         info = _RxInfo()
         bits = np.zeros(96 * nf, np.int32)
@@ -191,7 +211,7 @@ class Oracle:
         snr = np.ascontiguousarray(snr_db, np.float64)
         cnt = np.zeros((len(snr), NCOUNTERS), np.int64)
         pidx = np.zeros((len(snr), n_trials), np.int32) if dump_pidx else None
-        opts = self.rx_opts(mode)
+        opts = self.rx_opts(mode, self._frames if cfg.payload == PAYLOAD["message"] else 2)
         self.lib.orc_frame_sweep(C.byref(cfg), C.byref(opts), _p(snr), len(snr), first_trial, n_trials,
                                  _p(cnt), _p(pidx))
         return (cnt, pidx) if dump_pidx else cnt

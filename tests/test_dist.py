@@ -54,3 +54,32 @@ def test_two_rank_allreduce_equals_single(tmp_path, oracle, mode):
     got = np.load(out)
     ref = oracle.symbol_sweep(oracle.cfg(), snrs, 0, n)
     assert np.array_equal(got, ref)
+
+
+def _wl_worker(rank, world, port, out_path):
+    import sys
+    sys.path.insert(0, str(ROOT))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import ofdm_pkg
+    ofdm_pkg.load()
+    from ofdm_amd import abi, dist as odist
+    t = torch.zeros((2, 16), dtype=torch.int64)
+    t[:, abi.C_BITS] = 100 * (rank + 1)
+    t[:, abi.C_WL_MIN_Q] = torch.tensor([-3 << 20, -1 << 19]) * (rank + 1)      # rank 1 holds the minimum
+    t[:, abi.C_WL_MAX_Q] = torch.tensor([5 << 20, 1 << 18]) * (2 - rank)        # rank 0 holds the maximum
+    odist.allreduce_counters(t, word_stats=True)
+    if rank == 0:
+        np.save(out_path, t.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_word_stats_reduce_min_max(tmp_path):
+    """OFDM_C_WL_* slots are extremes: MIN / MAX over ranks, bits recomputed; everything else sums."""
+    out = tmp_path / "w.npy"
+    mp.spawn(_wl_worker, args=(2, _free_port(), str(out)), nprocs=2, join=True)
+    t = np.load(out)
+    assert list(t[:, 2]) == [300, 300]
+    assert list(t[:, 13]) == [-6 << 20, -1 << 20] and list(t[:, 14]) == [10 << 20, 1 << 19]
+    assert list(t[:, 15]) == [5, 1]           # max|.| 10 -> ceil(log2 10) + 1 = 5; 1.0 -> ceil(0) + 1 = 1
