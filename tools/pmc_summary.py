@@ -62,7 +62,8 @@ def main(argv):
     vals, _ = read_counters(d)
     trace = read_trace(d)
     summary = json.loads(out.read_text()) if out.exists() else {}
-    rx = "rx_ls_kernel" if "rx_ls_kernel" in vals else "rx_ideal_kernel"
+    # the receiver kernel of this run (symbol-mode LS / ideal, or frame mode)
+    rx = next(k for k in ("rx_ls_kernel", "rx_ideal_kernel", "frame_rx_kernel") if k in vals)
     c = {k: statistics.mean(v) for k, v in vals[rx].items()}
     t = trace.get(rx, {}).get("avg_ns", float("nan")) * 1e-9
     rd = 2.0 * c.get("FETCH_SIZE", float("nan")) * 1024
