@@ -69,6 +69,12 @@ __device__ __forceinline__ float2 box_muller(uint32_t x1, uint32_t x2) {
     return make_float2(r * __builtin_amdgcn_cosf(u2), r * __builtin_amdgcn_sinf(u2));
 }
 
+// The same four draws scaled by sigma, left as radius and angle terms so that each noisy sample
+// is one fma: sigma z = r (cos | sin), r = sqrt(K log2 u1) with K = -2 ln(2) sigma^2 folded under
+// the square root (sigma sqrt(-2 ln u1) = sqrt(-2 ln 2 sigma^2 log2 u1)).
+struct Noise4 { float r0, c0, s0, r1, c1, s1; };   // sigma (z0, z1, z2, z3) = (r0 c0, r0 s0, r1 c1, r1 s1)
+__device__ __forceinline__ float noise_k(float sigma) { return -1.38629436111989061883f * sigma * sigma; }
+
 // four N(0,1) draws of one Philox block
 struct Gauss4 { float z[4]; };
 __device__ __forceinline__ Gauss4 gauss4(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
@@ -78,6 +84,19 @@ __device__ __forceinline__ Gauss4 gauss4(uint32_t c0, uint32_t c1, uint32_t c2, 
     Gauss4 g;
     g.z[0] = a.x; g.z[1] = a.y; g.z[2] = b.x; g.z[3] = b.y;
     return g;
+}
+
+__device__ __forceinline__ Noise4 noise4(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
+                                         float K) {
+    const uint4 o = philox10(c0, c1, c2, c3, k0, k1);
+    const float u1a = fmaf((float)o.x, 0x1p-32f, 0x1p-33f), u2a = (float)o.y * 0x1p-32f;
+    const float u1b = fmaf((float)o.z, 0x1p-32f, 0x1p-33f), u2b = (float)o.w * 0x1p-32f;
+    Noise4 n;
+    n.r0 = __builtin_amdgcn_sqrtf(K * __builtin_amdgcn_logf(u1a));
+    n.r1 = __builtin_amdgcn_sqrtf(K * __builtin_amdgcn_logf(u1b));
+    n.c0 = __builtin_amdgcn_cosf(u2a); n.s0 = __builtin_amdgcn_sinf(u2a);
+    n.c1 = __builtin_amdgcn_cosf(u2b); n.s1 = __builtin_amdgcn_sinf(u2b);
+    return n;
 }
 
 // ------------------------------------------------------------------ twiddles

@@ -184,10 +184,11 @@ __device__ __forceinline__ void stage_group(const RxArgs &a, int64_t col0, float
 
 // Load + channel + AWGN for samples n0..n0+3, times (-1)^n (fft() = DFT of x(-1)^n, OFDM.c:314-318).
 // Noise sample at frame time t uses Gaussian t (real) or 2t, 2t+1 (complex) of the frame's stream
-// (DESIGN.md §3); AWGN is real-only as OFDM.c:651 really does (D7).
+// (DESIGN.md §3); AWGN is real-only as OFDM.c:651 really does (D7).  K = noise_k(sigma) (real) or
+// noise_k(sigma / sqrt2) (complex): each noisy component is one fma (Noise4).
 template <int NOISE, int CHAN, int N0, typename WS>
 __device__ __forceinline__ void rx_block(float2 (&x)[64], const WS &src, uint32_t f_lo, uint32_t f_hi,
-                                         uint32_t t0, uint32_t q, float sigma, uint32_t k0, uint32_t k1,
+                                         uint32_t t0, uint32_t q, float K, uint32_t k0, uint32_t k1,
                                          const float2 (&h)[4]) {
     // re-materialise per block: keeps LICM from hoisting 16 blocks' worth of addresses / round-1 products
     WS p = src;
@@ -195,15 +196,15 @@ __device__ __forceinline__ void rx_block(float2 (&x)[64], const WS &src, uint32_
     uint32_t flo = f_lo, fhi = f_hi, tb = t0;
     opaque(flo); opaque(fhi); opaque(tb);
     f_lo = flo; f_hi = fhi; t0 = tb;
-    float z[8];
+    float nr[8], nt[8];     // noise of component j = nr[j] * nt[j]
     if constexpr (NOISE == OFDM_NOISE_REAL) {
-        const Gauss4 g = gauss4(f_lo, f_hi, (t0 >> 2) + (N0 >> 2), STREAM_NOISE | q, k0, k1);
-        z[0] = g.z[0]; z[1] = g.z[1]; z[2] = g.z[2]; z[3] = g.z[3];
+        const Noise4 g = noise4(f_lo, f_hi, (t0 >> 2) + (N0 >> 2), STREAM_NOISE | q, k0, k1, K);
+        nr[0] = g.r0; nt[0] = g.c0; nr[1] = g.r0; nt[1] = g.s0; nr[2] = g.r1; nt[2] = g.c1; nr[3] = g.r1; nt[3] = g.s1;
     } else if constexpr (NOISE == OFDM_NOISE_COMPLEX) {
-        const Gauss4 g0 = gauss4(f_lo, f_hi, (t0 >> 1) + (N0 >> 1), STREAM_NOISE | q, k0, k1);
-        const Gauss4 g1 = gauss4(f_lo, f_hi, (t0 >> 1) + (N0 >> 1) + 1, STREAM_NOISE | q, k0, k1);
-        z[0] = g0.z[0]; z[1] = g0.z[1]; z[2] = g0.z[2]; z[3] = g0.z[3];
-        z[4] = g1.z[0]; z[5] = g1.z[1]; z[6] = g1.z[2]; z[7] = g1.z[3];
+        const Noise4 g0 = noise4(f_lo, f_hi, (t0 >> 1) + (N0 >> 1), STREAM_NOISE | q, k0, k1, K);
+        const Noise4 g1 = noise4(f_lo, f_hi, (t0 >> 1) + (N0 >> 1) + 1, STREAM_NOISE | q, k0, k1, K);
+        nr[0] = g0.r0; nt[0] = g0.c0; nr[1] = g0.r0; nt[1] = g0.s0; nr[2] = g0.r1; nt[2] = g0.c1; nr[3] = g0.r1; nt[3] = g0.s1;
+        nr[4] = g1.r0; nt[4] = g1.c0; nr[5] = g1.r0; nt[5] = g1.s0; nr[6] = g1.r1; nt[6] = g1.c1; nr[7] = g1.r1; nt[7] = g1.s1;
     }
     float2 c[7];
     if constexpr (CHAN == OFDM_CHAN_RAYLEIGH4) {
@@ -219,11 +220,10 @@ __device__ __forceinline__ void rx_block(float2 (&x)[64], const WS &src, uint32_
             y = cadd(cadd(cmul(h[0], c[3 + i]), cmul(h[1], c[2 + i])), cadd(cmul(h[2], c[1 + i]), cmul(h[3], c[i])));
         }
         if constexpr (NOISE == OFDM_NOISE_REAL) {
-            y.x = fmaf(sigma, z[i], y.x);
+            y.x = fmaf(nr[i], nt[i], y.x);
         } else if constexpr (NOISE == OFDM_NOISE_COMPLEX) {
-            const float sh = sigma * INV_SQRT2;
-            y.x = fmaf(sh, z[2 * i], y.x);
-            y.y = fmaf(sh, z[2 * i + 1], y.y);
+            y.x = fmaf(nr[2 * i], nt[2 * i], y.x);
+            y.y = fmaf(nr[2 * i + 1], nt[2 * i + 1], y.y);
         }
         if constexpr (n & 1) y = make_float2(-y.x, -y.y);
         x[n] = y;
@@ -235,12 +235,13 @@ template <int NOISE, int CHAN, typename WS>
 __device__ __forceinline__ void rx_window_stage1(float2 (&x)[64], const WS &src, uint32_t f_lo,
                                                  uint32_t f_hi, uint32_t t0, uint32_t q, float sigma,
                                                  uint32_t k0, uint32_t k1, const float2 (&h)[4]) {
+    const float K = noise_k(NOISE == OFDM_NOISE_COMPLEX ? sigma * INV_SQRT2 : sigma);
     static_for<0, 4>([&](auto gc) {
         constexpr int g = decltype(gc)::value;
-        rx_block<NOISE, CHAN, 4 * g>(x, src, f_lo, f_hi, t0, q, sigma, k0, k1, h);
-        rx_block<NOISE, CHAN, 16 + 4 * g>(x, src, f_lo, f_hi, t0, q, sigma, k0, k1, h);
-        rx_block<NOISE, CHAN, 32 + 4 * g>(x, src, f_lo, f_hi, t0, q, sigma, k0, k1, h);
-        rx_block<NOISE, CHAN, 48 + 4 * g>(x, src, f_lo, f_hi, t0, q, sigma, k0, k1, h);
+        rx_block<NOISE, CHAN, 4 * g>(x, src, f_lo, f_hi, t0, q, K, k0, k1, h);
+        rx_block<NOISE, CHAN, 16 + 4 * g>(x, src, f_lo, f_hi, t0, q, K, k0, k1, h);
+        rx_block<NOISE, CHAN, 32 + 4 * g>(x, src, f_lo, f_hi, t0, q, K, k0, k1, h);
+        rx_block<NOISE, CHAN, 48 + 4 * g>(x, src, f_lo, f_hi, t0, q, K, k0, k1, h);
         static_for<0, 4>([&](auto ic) { dif_stage1<false, 4 * g + decltype(ic)::value>(x); });
         sched_fence();
     });
