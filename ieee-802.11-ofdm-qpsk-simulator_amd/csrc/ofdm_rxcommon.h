@@ -135,6 +135,19 @@ __device__ __forceinline__ EqOut<2> ls_equalise(float2 Y) {
     return e;
 }
 
+// Equaliser objects for finish_symbol: operator()(Y, bin) -> EqOut, and prefetch<R>(x) called once
+// per FFT sub-block before its bins are consumed (LDS-crossbar fetches issued as one batch).
+template <typename F>
+struct EqFn {
+    F f;
+    template <int R>
+    __device__ __forceinline__ void prefetch(const float2 (&)[64]) {}
+    template <typename B>
+    __device__ __forceinline__ auto operator()(float2 Y, B b) { return f(Y, b); }
+};
+template <typename F>
+__device__ __forceinline__ EqFn<F> eq_fn(F f) { return EqFn<F>{f}; }
+
 // frame-level counters of one wave, reduced and added into the block's LDS slots
 struct FrameAcc {
     uint32_t bit_err = 0, frame_err = 0, axis = 0, post_finite = 0;

@@ -259,6 +259,7 @@ __device__ __forceinline__ void finish_symbol(float2 (&x)[64], const uint32_t (&
     static_for<0, 4>([&](auto rc) {
         constexpr int R = decltype(rc)::value;
         dif_sub16<false, R>(x);
+        Hof.template prefetch<R>(x);
         demap_sub<DUMP, R, KIND>(x, w, Hof, dump_eq, st);
         sched_fence();
     });
@@ -285,16 +286,33 @@ template <int CHAN>
 using LsGeom = StageGeom<CHAN, LS_GROUP_SYMS / 2, 1>;      // 42 data symbols + the 2T chunk per row
 static_assert(LS_ROW_F2 == 2 * (LS_GROUP_SYMS / 2 + 1), "LS staged row = 42 symbols + 2T (x2)");
 
-template <int BIN>
-__device__ __forceinline__ EqOut<2> ls_equalise_bp(float2 Y, uint32_t e_addr) {
-    // S[k] = F1[k] + F2[k] from the frame's E lane; Z = Y / (0.5 Lf S) = 2 Lf Y conj(S) / |S|^2
-    const float2 S = make_float2(__int_as_float(__builtin_amdgcn_ds_bpermute((int)e_addr, __float_as_int(Y.x))),
-                                 __int_as_float(__builtin_amdgcn_ds_bpermute((int)e_addr, __float_as_int(Y.y))));
-    EqOut<2> e;
-    e.r = __builtin_amdgcn_rcpf(fmaf(S.x, S.x, S.y * S.y));
-    e.u = cscale(cmulc(Y, S), (float)ltf_sign(BIN));
-    return e;
-}
+// S[k] = F1[k] + F2[k] from the frame's E lane (ds_bpermute), fetched for a whole FFT sub-block at
+// once; Z = Y / (0.5 Lf S) = 2 Lf Y conj(S) / |S|^2
+struct LsBpermuteEq {
+    uint32_t e_addr;
+    float2 S[16];
+    template <int R>
+    __device__ __forceinline__ void prefetch(const float2 (&x)[64]) {
+        static_for<0, 16>([&](auto kc) {
+            constexpr int bin = 4 * decltype(kc)::value + R;
+            if constexpr (data_index(bin) >= 0) {
+                const float2 Y = x[digit_rev4(bin)];
+                S[decltype(kc)::value] = make_float2(
+                    __int_as_float(__builtin_amdgcn_ds_bpermute((int)e_addr, __float_as_int(Y.x))),
+                    __int_as_float(__builtin_amdgcn_ds_bpermute((int)e_addr, __float_as_int(Y.y))));
+            }
+        });
+    }
+    template <typename B>
+    __device__ __forceinline__ EqOut<2> operator()(float2 Y, B) const {
+        constexpr int bin = B::value;
+        const float2 Sb = S[bin >> 2];
+        EqOut<2> e;
+        e.r = __builtin_amdgcn_rcpf(fmaf(Sb.x, Sb.x, Sb.y * Sb.y));
+        e.u = cscale(cmulc(Y, Sb), (float)ltf_sign(bin));
+        return e;
+    }
+};
 
 template <int NOISE, int CHAN, bool DUMP>
 __global__ __launch_bounds__(256, OFDM_RX_LS_WAVES) void rx_ls_kernel(RxArgs a) {
@@ -359,7 +377,8 @@ __global__ __launch_bounds__(256, OFDM_RX_LS_WAVES) void rx_ls_kernel(RxArgs a) 
                     dump_bits = a.dump_bits + r * 3;
                 }
             }
-            auto Hof = [&](float2 Y, auto binc) { return ls_equalise_bp<decltype(binc)::value>(Y, e_addr); };
+            LsBpermuteEq Hof;
+            Hof.e_addr = e_addr;
             auto partner = [&](uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_bpermute((int)d1_addr, (int)v); };
             finish_symbol<DUMP, 2>(x, wq, Hof, partner, dump_eq, dump_bits, role == 1 && valid, sacc[q]);
         }
@@ -437,7 +456,8 @@ __global__ __launch_bounds__(256, OFDM_RX_IDEAL_WAVES) void rx_ideal_kernel(RxAr
                 return e;
             };
             auto partner = [](uint32_t v) { return dpp_u<DPP_QUAD_XOR1>(v); };
-            finish_symbol<DUMP, KIND>(x, wq, Hof, partner, dump_eq, dump_bits, d == 0 && valid, sacc[q]);
+            auto eq = eq_fn(Hof);
+            finish_symbol<DUMP, KIND>(x, wq, eq, partner, dump_eq, dump_bits, d == 0 && valid, sacc[q]);
         }
         __syncthreads();                                   // every wave is done with the group
     }
