@@ -107,7 +107,8 @@ def main():
     from ofdm_amd import abi, dist as odist
 
     rank, world, local = odist.env_rank_world()
-    distributed = world > 1
+    # under torch.distributed.run (RANK set) the RCCL group is formed even for one rank
+    distributed = world > 1 or "RANK" in os.environ
     if distributed:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
