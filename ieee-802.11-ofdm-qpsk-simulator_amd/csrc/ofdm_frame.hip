@@ -67,7 +67,19 @@ struct FrameArgs {
     float2 *dbg_frame;              // fr_len(n_data) samples after fine CFO
     float taps[21];
     float sigma[OFDM_MAX_SNR];
+    unsigned long long *stamps;     // OFDM_FRAME_STAMPS builds: cycles per receiver phase [8]
 };
+
+#ifdef OFDM_FRAME_STAMPS   // diagnostic build: s_memtime per phase, summed over the grid
+#define FR_STAMP(k)                                                                  \
+    do {                                                                             \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                  \
+        if (threadIdx.x == 0) stamp_acc[k] += t_ - stamp_t;                          \
+        stamp_t = t_;                                                                \
+    } while (0)
+#else
+#define FR_STAMP(k) do { } while (0)
+#endif
 
 // ======================================================================== K4a: waveform
 template <int CONV>
@@ -285,6 +297,10 @@ __global__ __launch_bounds__(64) void frame_rx_kernel(FrameArgs a) {
     }
     const int chunk = (Lc + 63) / 64;           // detection positions per lane (< 300: one front each)
     const int64_t items = a.n_trials * a.n_snr;
+#ifdef OFDM_FRAME_STAMPS
+    unsigned long long stamp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long stamp_t = __builtin_amdgcn_s_memtime();
+#endif
     for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
         const int q = (int)(it % a.n_snr);
         const int64_t ti = it / a.n_snr;
@@ -302,23 +318,38 @@ __global__ __launch_bounds__(64) void frame_rx_kernel(FrameArgs a) {
         } else {
             const int b0 = rx_start >> 2, b1 = (rx_start + L - 1) >> 2;
             // Gaussian k of the trial's stream goes to waveform sample k (as if Transmission_Over_Air
-            // had drawn the whole waveform); only the captured samples are ever evaluated
-            for (int b = b0 + lane; b <= b1; b += 64) {
-                Gauss4 g;
-                if (a.noise == OFDM_NOISE_REAL) g = gauss4(t_lo, t_hi, (uint32_t)b, STREAM_NOISE | qs, a.k0, a.k1);
+            // had drawn the whole waveform); only the captured samples are ever evaluated.  Four
+            // Philox blocks per lane per pass, their waveform loads issued first.
+            for (int bb = b0 + lane; bb <= b1; bb += 256) {
+                float2 v[4][4];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int n = 4 * b + j - rx_start;
-                    if (n >= 0 && n < L) {
-                        float2 v = a.wave[4 * b + j];
-                        if (a.noise == OFDM_NOISE_REAL) v.x = fmaf(sigma, g.z[j], v.x);   // real-only (D7)
-                        r[n] = v;
+                for (int u = 0; u < 4; ++u)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int k = 4 * (bb + 64 * u) + j;
+                        v[u][j] = (bb + 64 * u <= b1 && k < a.wave_len) ? a.wave[k] : make_float2(0.f, 0.f);
+                    }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int b = bb + 64 * u;
+                    if (b > b1) break;
+                    Gauss4 g;
+                    if (a.noise == OFDM_NOISE_REAL) g = gauss4(t_lo, t_hi, (uint32_t)b, STREAM_NOISE | qs, a.k0, a.k1);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int n = 4 * b + j - rx_start;
+                        if (n >= 0 && n < L) {
+                            float2 w = v[u][j];
+                            if (a.noise == OFDM_NOISE_REAL) w.x = fmaf(sigma, g.z[j], w.x);   // real-only (D7)
+                            r[n] = w;
+                        }
                     }
                 }
             }
         }
         for (int i = lane; i < cross_words(L); i += 64) cross[i] = 0ull;
         __syncthreads();
+        FR_STAMP(0);                                           // capture + noise
 
         // ---- Word_Optimization_Analysis(Rx_filter_signal) (OFDM.c:38-73, 962-967): the full RRC
         // matched filter of the capture, min / max over real and imaginary parts (opt-in) ----
@@ -347,11 +378,14 @@ __global__ __launch_bounds__(64) void frame_rx_kernel(FrameArgs a) {
         }
 
         // ---- Packet_Detection (OFDM.c:659-683): M[n] = |sum r[n+k] r[n+k+16]|^2 / (sum |r[n+k+16]|^2)^2,
-        // k < 32, no conjugate, on the UNFILTERED capture; sliding sums over each lane's chunk, the
-        // > 0.75 crossings (Packet_Selection's threshold, OFDM.c:687) kept as a bit mask ----
+        // k < 32, no conjugate, on the UNFILTERED capture; sliding sums over each lane's chunk with the
+        // LDS reads issued 8 positions at a time.  M > 0.75 (OFDM.c:687, 695) is tested as
+        // num > 0.75 den, which keeps the division's 0/0 -> false and x/0 -> true outcomes. ----
         const int n0 = lane * chunk, n1 = min(n0 + chunk, Lc);
+        int first = -1, last = -1;                  // first / last crossing in this lane's chunk
         if (n0 < n1) {
             float sx = 0.f, sy = 0.f, pw = 0.f;
+#pragma unroll 8
             for (int k = 0; k < 32; ++k) {
                 const float2 u = r[n0 + k], v = r[n0 + k + 16];
                 sx += u.x * v.x - u.y * v.y;
@@ -359,66 +393,89 @@ __global__ __launch_bounds__(64) void frame_rx_kernel(FrameArgs a) {
                 pw += v.x * v.x + v.y * v.y;
             }
             unsigned long long word = 0ull;
-            for (int n = n0; n < n1; ++n) {
-                const float M = (sx * sx + sy * sy) / (pw * pw);
-                if (M > 0.75f) word |= 1ull << (n & 63);
-                if (a.dbg_corr && it == 0) a.dbg_corr[n] = M;
-                if ((n & 63) == 63 || n + 1 == n1) {
-                    if (word) atomicOr(&cross[n >> 6], word);
-                    word = 0ull;
+            for (int nb = n0; nb < n1; nb += 8) {
+                float2 o0[8], o1[8], i0[8], i1[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {           // reads past the capture land in fr/cross: unused
+                    o0[k] = r[nb + k]; o1[k] = r[nb + k + 16]; i0[k] = r[nb + k + 32]; i1[k] = r[nb + k + 48];
                 }
-                if (n + 1 < n1) {
-                    const float2 o0 = r[n], o1 = r[n + 16], i0 = r[n + 32], i1 = r[n + 48];
-                    sx += (i0.x * i1.x - i0.y * i1.y) - (o0.x * o1.x - o0.y * o1.y);
-                    sy += (i0.x * i1.y + i0.y * i1.x) - (o0.x * o1.y + o0.y * o1.x);
-                    pw += (i1.x * i1.x + i1.y * i1.y) - (o1.x * o1.x + o1.y * o1.y);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const int n = nb + k;
+                    if (n >= n1) break;
+                    const float num = sx * sx + sy * sy, den = pw * pw;
+                    if (a.dbg_corr && it == 0) a.dbg_corr[n] = num / den;
+                    if (num > 0.75f * den) {
+                        word |= 1ull << (n & 63);
+                        if (first < 0) first = n;
+                        last = n;
+                    }
+                    if ((n & 63) == 63 || n + 1 == n1) {
+                        if (word) atomicOr(&cross[n >> 6], word);
+                        word = 0ull;
+                    }
+                    sx += (i0[k].x * i1[k].x - i0[k].y * i1[k].y) - (o0[k].x * o1[k].x - o0[k].y * o1[k].y);
+                    sy += (i0[k].x * i1[k].y + i0[k].y * i1[k].x) - (o0[k].x * o1[k].y + o0[k].y * o1[k].x);
+                    pw += (i1[k].x * i1[k].x + i1[k].y * i1[k].y) - (o1[k].x * o1[k].x + o1[k].y * o1[k].y);
                 }
             }
         }
-        __syncthreads();
 
-        // ---- Packet_Selection (OFDM.c:685-771): a crossing i is a front iff i - prev > 300 with
-        // prev = previous crossing or -1, i.e. i >= 300 and no crossing in [i-300, i-1]; the first
-        // front x with a later front and M[front+230] > 0.75 gives packet_idx = front + 11.  Fronts
-        // are > 300 apart, so a lane's chunk (< 300 positions) holds at most one. ----
-        int front = -1;
-        for (int wd = n0 >> 6; n0 < n1 && wd <= ((n1 - 1) >> 6) && front < 0; ++wd) {
-            unsigned long long m = cross[wd];
-            if (wd == (n0 >> 6)) m &= ~0ull << (n0 & 63);
-            if (wd == ((n1 - 1) >> 6) && ((n1 - 1) & 63) != 63) m &= (1ull << (((n1 - 1) & 63) + 1)) - 1ull;
-            for (; m; m &= m - 1) {
-                const int i = (wd << 6) + __builtin_ctzll(m);
-                if (i >= 300 && !any_bits(cross, i - 300, i - 1)) { front = i; break; }
-            }
+        // ---- Packet_Selection (OFDM.c:685-771): crossing idx[j] is a front iff idx[j] - idx[j-1] > 300
+        // (idx[-1] = -1).  Fronts are > 300 apart and a chunk is < 300 positions, so only a lane's
+        // first crossing can be one, and its predecessor is the last crossing of the earlier chunks:
+        // an exclusive prefix max over lanes.  The first front x with a later front and
+        // M[front+230] > 0.75 gives packet_idx = front + len_RRC_rx + 1; otherwise 0 (OFDM.c:752-761). ----
+        int pm = last;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(pm, o, 64);
+            if (lane >= o) pm = max(pm, t);
         }
+        int prev = __shfl_up(pm, 1, 64);
+        if (lane == 0) prev = -1;
+        const int front = (first >= 0 && first - prev > 300) ? first : -1;
+        __syncthreads();                            // every crossing word is in LDS
+        FR_STAMP(1);                                           // packet detection
         const bool valid = front >= 0 && front + 230 < Lc && bit_at(cross, front + 230);
         const int maxf = wave_max_i(front);
         const int cand = wave_min_i((valid && front < maxf) ? front : 0x7fffffff);
         const bool sync_fail = cand == 0x7fffffff;
         const int p = sync_fail ? 0 : cand + 10 + 1;           // len_RRC_rx + 1 (OFDM.c:758)
+        FR_STAMP(2);                                           // packet selection
 
-        // ---- RRC matched filter at the down-sampled instants p + 2i (OFDM.c:965, 992-996) ----
+        // ---- RRC matched filter at the down-sampled instants p + 2i (OFDM.c:965, 992-996): a lane
+        // takes 8 consecutive outputs, i.e. one 35-sample window of the capture held in registers ----
         bool oob_l = false;
-        for (int i = lane; i < nfr; i += 64) {
-            const int n = p + 2 * i;
-            float2 v = make_float2(0.f, 0.f);
-            if (n >= L + 20) {
-                oob_l = true;                                    // the reference reads past its buffer
-            } else {
+        for (int ib = 8 * lane; ib < nfr; ib += 512) {
+            const int nb = p + 2 * ib - 20;             // first capture sample the 8 outputs touch
+            float2 win[35];
 #pragma unroll
-                for (int j = 0; j < 21; ++j) {
-                    const int m = n - j;
-                    if (m >= 0 && m < L) {
-                        const float2 x = r[m];
+            for (int k = 0; k < 35; ++k) {
+                const int m = nb + k;
+                win[k] = (m >= 0 && m < L) ? r[m] : make_float2(0.f, 0.f);   // Convolution zero-pads
+            }
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const int i = ib + t;
+                if (i >= nfr) break;
+                float2 v = make_float2(0.f, 0.f);
+                if (p + 2 * i >= L + 20) {
+                    oob_l = true;                                // the reference reads past its buffer
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 21; ++j) {
+                        const float2 x = win[2 * t + 20 - j];
                         v.x = fmaf(x.x, a.taps[j], v.x);
                         v.y = fmaf(x.y, a.taps[j], v.y);
                     }
                 }
+                fr[i] = v;
             }
-            fr[i] = v;
         }
         const bool oob = __any(oob_l);
         __syncthreads();
+        FR_STAMP(3);                                           // matched filter + down-sample
 
         // ---- Coarse CFO (OFDM.c:773-804): 16-lag autocorrelation of the short preamble ----
         float px = 0.f, py = 0.f;
@@ -440,6 +497,7 @@ __global__ __launch_bounds__(64) void frame_rx_kernel(FrameArgs a) {
         for (int i = lane; i < nfr; i += 64) fr[i] = cfo_rot(fr[i], ff * TS, i);
         __syncthreads();
         if (a.dbg_frame && it == 0) for (int i = lane; i < nfr; i += 64) a.dbg_frame[i] = fr[i];
+        FR_STAMP(4);                                           // coarse + fine CFO
 
         // ---- LS estimate + CP strip + fft + ZF + slicer + demap (OFDM.c:830-1100).  Quad k carries
         // {LTF1, LTF2, D_2k, D_2k+1}: the estimate is formed inside each quad (two broadcasts) ----
@@ -454,14 +512,21 @@ __global__ __launch_bounds__(64) void frame_rx_kernel(FrameArgs a) {
             const float2 v = fr[w0 + n];
             x[n] = (n & 1) ? make_float2(-v.x, -v.y) : v;        // fft() = DFT(x (-1)^n)
         });
+#ifndef OFDM_FRAME_NO_FFT   // profiling switch: time the sync phases alone
         fft64<false>(x);
+#endif
         const uint32_t w[3] = {a.table[3 * dsc], a.table[3 * dsc + 1], a.table[3 * dsc + 2]};
         SymState st;
         sym_init(st);
         const bool dump = a.dbg_eq && it == 0 && dlane;
         float2 *deq = dump ? a.dbg_eq + 48 * dsym : nullptr;
         auto Hof = [&](float2 Y, auto binc) { return ls_equalise<decltype(binc)::value>(Y); };
+#ifndef OFDM_FRAME_NO_FFT
         static_for<0, 4>([&](auto rc) { demap_sub<true, decltype(rc)::value, 2>(x, w, Hof, deq, st); });
+#else
+        st.evm_pre = x[5].x;
+#endif
+        FR_STAMP(5);                                           // FFT + LS + demap
         const float fe = wave_sum_f(dlane ? finish_evm<2>(st) : 0.f);
         const uint32_t ferr = wave_sum_u32(dlane ? st.be : 0u), fax = wave_sum_u32(dlane ? st.ax : 0u);
         if (lane == 0) {
@@ -491,7 +556,12 @@ __global__ __launch_bounds__(64) void frame_rx_kernel(FrameArgs a) {
             a.dbg_bits[3 * dsym] = st.d[0]; a.dbg_bits[3 * dsym + 1] = st.d[1]; a.dbg_bits[3 * dsym + 2] = st.d[2];
         }
         __syncthreads();
+        FR_STAMP(6);                                           // counters
     }
+#ifdef OFDM_FRAME_STAMPS
+    if (threadIdx.x == 0 && a.stamps)
+        for (int k = 0; k < 7; ++k) atomicAdd(&a.stamps[k], stamp_acc[k]);
+#endif
     __syncthreads();
     for (int i = lane; i < a.n_snr * 9; i += 64) {
         const int q = i / 9, k = i % 9;
@@ -749,10 +819,28 @@ int ofdm_frame_sweep(ofdm_ctx *ctx, const ofdm_cfg *cfg, const ofdm_rx_opts *opt
             a.sigma[q] = (float)std::sqrt(c->wave_power / std::pow(10.0, snr_db[q0 + q] / 10.0));
         if (n_trials == 0) continue;
         const size_t lds = frame_lds_bytes(a.cap_len, a.n_data, a.n_snr);
+#ifdef OFDM_FRAME_STAMPS
+        unsigned long long *dst = nullptr;
+        HIPOK(hipMalloc(&dst, 64));
+        HIPOK(hipMemset(dst, 0, 64));
+        a.stamps = dst;
+#endif
         c->tic(Ctx::K_FRAME);
         hipLaunchKernelGGL(frame_rx_kernel, dim3(frame_grid(c, n_trials * a.n_snr, lds)), dim3(64), lds, c->stream, a);
         c->toc();
         HIPOK(hipGetLastError());
+#ifdef OFDM_FRAME_STAMPS
+        unsigned long long hs[8];
+        HIPOK(hipMemcpy(hs, dst, 64, hipMemcpyDeviceToHost));
+        hipFree(dst);
+        static const char *names[7] = {"capture+noise", "detection", "selection", "matched filter", "cfo",
+                                       "fft+ls+demap", "counters"};
+        double tot = 0;
+        for (int k = 0; k < 7; ++k) tot += (double)hs[k];
+        for (int k = 0; k < 7; ++k)
+            fprintf(stderr, "frame stamp %-15s %6.2f%%  %.0f cycles/item\n", names[k], 100.0 * hs[k] / tot,
+                    (double)hs[k] / (double)(n_trials * a.n_snr));
+#endif
     }
     HIPOK(hipMemcpyAsync(counters, c->d_cnt, cbytes, hipMemcpyDeviceToHost, c->stream));
     if (dp) HIPOK(hipMemcpyAsync(packet_idx, dp, pbytes, hipMemcpyDeviceToHost, c->stream));
