@@ -68,6 +68,11 @@ struct FrameArgs {
     float taps[21];
     float sigma[OFDM_MAX_SNR];
     unsigned long long *stamps;     // OFDM_FRAME_STAMPS builds: cycles per receiver phase [8]
+    // sync -> symbol hand-off (one chunk of items; item g = trial (g / n_snr), SNR (g % n_snr))
+    int64_t item0, n_items;         // first global item of the chunk, items in it
+    float2 *win;                    // [n_items][2 + n_data][64]: LTF1, LTF2, data windows after CFO
+    int4 *info;                     // [n_items]: packet_idx, sync_fail, oob, rx_start
+    int32_t add_totals;             // 1 on the last chunk: add frames / symbols / bits / terms
 };
 
 #ifdef OFDM_FRAME_STAMPS   // diagnostic build: s_memtime per phase, summed over the grid
@@ -265,89 +270,115 @@ __device__ __forceinline__ float2 cfo_rot(float2 v, double f_ts, int i) {
     return make_float2(v.x * c - v.y * s, v.x * s + v.y * c);
 }
 
+// ---------------------------------------------------------------- K4b: sync (one block per item)
 // LDS image of one trial (dynamic shared memory, sized per launch by frame_lds_bytes)
-struct FrameLds {
-    float2 *r;                  // capture [cap_len]
-    float2 *fr;                 // down-sampled frame [fr_len(n_data)]
-    unsigned long long *cross;  // Packet_Detection threshold crossings, 1 bit per position
-    unsigned long long *acc;    // [n_snr][ACC_SLOTS] per-SNR block accumulators
-};
-constexpr int ACC_SLOTS = 12;   // 9 counter sums + word-length min / max (q20) + pad
+constexpr int SYNC_THREADS = 128;   // two waves share each trial's latency-bound phases
+constexpr int ACC_SLOTS = 12;       // per-SNR block accumulators: 9 counter sums + word-length min / max
 __host__ __device__ inline int cross_words(int cap_len) { return (cap_len - 47 + 63) / 64 + 1; }
+// capture region: cap_len + 8 samples, the capture starting at sample (rx_start & 3) so that every
+// Philox block of 4 samples is a 16-byte aligned pair of ds_write_b128
+__host__ __device__ inline int cap_region(int cap_len) { return (cap_len + 8 + 1) & ~1; }
 __host__ __device__ inline size_t frame_lds_bytes(int cap_len, int n_data, int n_snr) {
-    return (size_t)cap_len * 8 + (size_t)fr_len(n_data) * 8 + (size_t)cross_words(cap_len) * 8 +
-           (size_t)n_snr * ACC_SLOTS * 8;
+    return (size_t)cap_region(cap_len) * 8 + (size_t)fr_len(n_data) * 8 + (size_t)cross_words(cap_len) * 8 +
+           (size_t)n_snr * ACC_SLOTS * 8 + 64;
 }
 
-__global__ __launch_bounds__(64) void frame_rx_kernel(FrameArgs a) {
+// block-wide reductions over the two waves (scratch: 2 slots in `red`)
+__device__ __forceinline__ float block_sum_f(float v, float *red) {
+    v = wave_sum_f(v);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    return red[0] + red[1];
+}
+__device__ __forceinline__ int block_max_i(int v, int *red) {
+    v = wave_max_i(v);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    return max(red[0], red[1]);
+}
+__device__ __forceinline__ int block_min_i(int v, int *red) {
+    v = wave_min_i(v);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    return min(red[0], red[1]);
+}
+
+__global__ __launch_bounds__(SYNC_THREADS) void frame_sync_kernel(FrameArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
     const int L = a.cap_len, Lc = L - 47;       // Packet_Detection length (OFDM.c:663)
     const int nfr = fr_len(a.n_data);
-    FrameLds s;
-    s.r = reinterpret_cast<float2 *>(smem);
-    s.fr = s.r + L;
-    s.cross = reinterpret_cast<unsigned long long *>(s.fr + nfr);
-    s.acc = s.cross + cross_words(L);
-    float2 *r = s.r, *fr = s.fr;
-    unsigned long long *cross = s.cross;
-    const int lane = threadIdx.x;
-    for (int i = lane; i < a.n_snr * ACC_SLOTS; i += 64) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    float2 *rbase = reinterpret_cast<float2 *>(smem);
+    float2 *fr = rbase + cap_region(L);
+    unsigned long long *cross = reinterpret_cast<unsigned long long *>(fr + nfr);
+    unsigned long long *acc = cross + cross_words(L);
+    float *redf = reinterpret_cast<float *>(acc + a.n_snr * ACC_SLOTS);
+    int *redi = reinterpret_cast<int *>(redf + 4);
+    for (int i = tid; i < a.n_snr * ACC_SLOTS; i += SYNC_THREADS) {
         const int k = i % ACC_SLOTS;
-        s.acc[i] = k == 10 ? (unsigned long long)INT64_MAX : k == 11 ? (unsigned long long)INT64_MIN : 0ull;
+        acc[i] = k == 10 ? (unsigned long long)INT64_MAX : k == 11 ? (unsigned long long)INT64_MIN : 0ull;
     }
-    const int chunk = (Lc + 63) / 64;           // detection positions per lane (< 300: one front each)
-    const int64_t items = a.n_trials * a.n_snr;
+    // detection positions per lane (< 300, <= 64); odd, so the lanes' 8-byte LDS reads fall in
+    // distinct banks
+    const int chunk = ((Lc + SYNC_THREADS - 1) / SYNC_THREADS) | 1;
 #ifdef OFDM_FRAME_STAMPS
     unsigned long long stamp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long stamp_t = __builtin_amdgcn_s_memtime();
 #endif
-    for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
-        const int q = (int)(it % a.n_snr);
-        const int64_t ti = it / a.n_snr;
+    for (int64_t i = blockIdx.x; i < a.n_items; i += gridDim.x) {
+        const int64_t g = a.item0 + i;
+        const int q = (int)(g % a.n_snr);
+        const int64_t ti = g / a.n_snr;
         const uint64_t t = a.first_trial + (uint64_t)ti;
         const uint32_t t_lo = (uint32_t)t, t_hi = (uint32_t)(t >> 32), qs = (uint32_t)(a.q_base + q);
         const float sigma = a.sigma[q];
+        const bool first_item = g == 0;
         // ---- capture window (OFDM.c:945-955) + AWGN ----
         int rx_start = a.fixed_start;
         if (rx_start < 0) {
             const uint4 o = philox10(t_lo, t_hi, 0u, STREAM_START | qs, a.k0, a.k1);
             rx_start = (int)(o.x % (uint32_t)(a.wave_len - L));
         }
-        if (a.ext && it == 0) {
-            for (int n = lane; n < L; n += 64) r[n] = a.ext[n];
+        float2 *r = rbase + (rx_start & 3);             // r[n] = capture sample n
+        if (a.ext && first_item) {
+            for (int n = tid; n < L; n += SYNC_THREADS) r[n] = a.ext[n];
         } else {
             const int b0 = rx_start >> 2, b1 = (rx_start + L - 1) >> 2;
             // Gaussian k of the trial's stream goes to waveform sample k (as if Transmission_Over_Air
             // had drawn the whole waveform); only the captured samples are ever evaluated.  Four
             // Philox blocks per lane per pass, their waveform loads issued first.
-            for (int bb = b0 + lane; bb <= b1; bb += 256) {
+            for (int bb = b0 + tid; bb <= b1; bb += 4 * SYNC_THREADS) {
                 float2 v[4][4];
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
-                        const int k = 4 * (bb + 64 * u) + j;
-                        v[u][j] = (bb + 64 * u <= b1 && k < a.wave_len) ? a.wave[k] : make_float2(0.f, 0.f);
+                        const int b = bb + SYNC_THREADS * u, k = 4 * b + j;
+                        v[u][j] = (b <= b1 && k < a.wave_len) ? a.wave[k] : make_float2(0.f, 0.f);
                     }
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
-                    const int b = bb + 64 * u;
+                    const int b = bb + SYNC_THREADS * u;
                     if (b > b1) break;
-                    Gauss4 g;
-                    if (a.noise == OFDM_NOISE_REAL) g = gauss4(t_lo, t_hi, (uint32_t)b, STREAM_NOISE | qs, a.k0, a.k1);
+                    Gauss4 gz;
+                    if (a.noise == OFDM_NOISE_REAL) gz = gauss4(t_lo, t_hi, (uint32_t)b, STREAM_NOISE | qs, a.k0, a.k1);
+                    float2 w[4];
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
-                        const int n = 4 * b + j - rx_start;
-                        if (n >= 0 && n < L) {
-                            float2 w = v[u][j];
-                            if (a.noise == OFDM_NOISE_REAL) w.x = fmaf(sigma, g.z[j], w.x);   // real-only (D7)
-                            r[n] = w;
-                        }
+                        w[j] = v[u][j];
+                        if (a.noise == OFDM_NOISE_REAL) w[j].x = fmaf(sigma, gz.z[j], w[j].x);   // real-only (D7)
                     }
+                    // samples of the block outside [0, L) land in the region's slack, never read as capture
+                    float4 *d4 = reinterpret_cast<float4 *>(rbase + 4 * (b - b0));
+                    d4[0] = make_float4(w[0].x, w[0].y, w[1].x, w[1].y);
+                    d4[1] = make_float4(w[2].x, w[2].y, w[3].x, w[3].y);
                 }
             }
         }
-        for (int i = lane; i < cross_words(L); i += 64) cross[i] = 0ull;
+        for (int k = tid; k < cross_words(L); k += SYNC_THREADS) cross[k] = 0ull;
         __syncthreads();
         FR_STAMP(0);                                           // capture + noise
 
@@ -355,7 +386,7 @@ __global__ __launch_bounds__(64) void frame_rx_kernel(FrameArgs a) {
         // matched filter of the capture, min / max over real and imaginary parts (opt-in) ----
         if (a.word_stats) {
             float mn = 1e9f, mx = -1e9f;
-            for (int k = lane; k < L + 20; k += 64) {
+            for (int k = tid; k < L + 20; k += SYNC_THREADS) {
                 float2 v = make_float2(0.f, 0.f);
 #pragma unroll
                 for (int j = 0; j < 21; ++j) {
@@ -370,10 +401,14 @@ __global__ __launch_bounds__(64) void frame_rx_kernel(FrameArgs a) {
             }
             mn = wave_min_f(mn);
             mx = wave_max_f(mx);
-            if (lane == 0) {
-                unsigned long long *sl = s.acc + q * ACC_SLOTS;
-                sl[10] = (unsigned long long)min((long long)sl[10], (long long)__float2ll_rn(mn * (float)OFDM_EVM_Q_SCALE));
-                sl[11] = (unsigned long long)max((long long)sl[11], (long long)__float2ll_rn(mx * (float)OFDM_EVM_Q_SCALE));
+            __syncthreads();
+            if (lane == 0) { redf[2 * (tid >> 6)] = mn; redf[2 * (tid >> 6) + 1] = mx; }
+            __syncthreads();
+            if (tid == 0) {
+                const float bmn = fminf(redf[0], redf[2]), bmx = fmaxf(redf[1], redf[3]);
+                unsigned long long *sl = acc + q * ACC_SLOTS;
+                sl[10] = (unsigned long long)min((long long)sl[10], (long long)__float2ll_rn(bmn * (float)OFDM_EVM_Q_SCALE));
+                sl[11] = (unsigned long long)max((long long)sl[11], (long long)__float2ll_rn(bmx * (float)OFDM_EVM_Q_SCALE));
             }
         }
 
@@ -381,8 +416,9 @@ __global__ __launch_bounds__(64) void frame_rx_kernel(FrameArgs a) {
         // k < 32, no conjugate, on the UNFILTERED capture; sliding sums over each lane's chunk with the
         // LDS reads issued 8 positions at a time.  M > 0.75 (OFDM.c:687, 695) is tested as
         // num > 0.75 den, which keeps the division's 0/0 -> false and x/0 -> true outcomes. ----
-        const int n0 = lane * chunk, n1 = min(n0 + chunk, Lc);
+        const int n0 = tid * chunk, n1 = min(n0 + chunk, Lc);
         int first = -1, last = -1;                  // first / last crossing in this lane's chunk
+        unsigned long long cmask = 0ull;            // crossing n at bit n - n0 (chunk <= 64)
         if (n0 < n1) {
             float sx = 0.f, sy = 0.f, pw = 0.f;
 #pragma unroll 8
@@ -392,7 +428,6 @@ __global__ __launch_bounds__(64) void frame_rx_kernel(FrameArgs a) {
                 sy += u.x * v.y + u.y * v.x;
                 pw += v.x * v.x + v.y * v.y;
             }
-            unsigned long long word = 0ull;
             for (int nb = n0; nb < n1; nb += 8) {
                 float2 o0[8], o1[8], i0[8], i1[8];
 #pragma unroll
@@ -400,187 +435,250 @@ __global__ __launch_bounds__(64) void frame_rx_kernel(FrameArgs a) {
                     o0[k] = r[nb + k]; o1[k] = r[nb + k + 16]; i0[k] = r[nb + k + 32]; i1[k] = r[nb + k + 48];
                 }
 #pragma unroll
-                for (int k = 0; k < 8; ++k) {
+                for (int k = 0; k < 8; ++k) {           // branch-free: positions >= n1 are masked off
                     const int n = nb + k;
-                    if (n >= n1) break;
                     const float num = sx * sx + sy * sy, den = pw * pw;
-                    if (a.dbg_corr && it == 0) a.dbg_corr[n] = num / den;
-                    if (num > 0.75f * den) {
-                        word |= 1ull << (n & 63);
-                        if (first < 0) first = n;
-                        last = n;
-                    }
-                    if ((n & 63) == 63 || n + 1 == n1) {
-                        if (word) atomicOr(&cross[n >> 6], word);
-                        word = 0ull;
-                    }
+                    const bool cr = n < n1 && num > 0.75f * den;
+                    cmask |= cr ? 1ull << (n - n0) : 0ull;
+                    first = (cr && first < 0) ? n : first;
+                    last = cr ? n : last;
                     sx += (i0[k].x * i1[k].x - i0[k].y * i1[k].y) - (o0[k].x * o1[k].x - o0[k].y * o1[k].y);
                     sy += (i0[k].x * i1[k].y + i0[k].y * i1[k].x) - (o0[k].x * o1[k].y + o0[k].y * o1[k].x);
                     pw += (i1[k].x * i1[k].x + i1[k].y * i1[k].y) - (o1[k].x * o1[k].x + o1[k].y * o1[k].y);
                 }
+            }
+            if (cmask) {
+                atomicOr(&cross[n0 >> 6], cmask << (n0 & 63));
+                if ((n0 & 63) + chunk > 64) atomicOr(&cross[(n0 >> 6) + 1], cmask >> (64 - (n0 & 63)));
+            }
+        }
+        if (a.dbg_corr && first_item) {             // Corr_Out for ofdm_receiver's parity dump
+            for (int n = tid; n < Lc; n += SYNC_THREADS) {
+                float sx = 0.f, sy = 0.f, pw = 0.f;
+                for (int k = 0; k < 32; ++k) {
+                    const float2 u = r[n + k], v = r[n + k + 16];
+                    sx += u.x * v.x - u.y * v.y;
+                    sy += u.x * v.y + u.y * v.x;
+                    pw += v.x * v.x + v.y * v.y;
+                }
+                a.dbg_corr[n] = (sx * sx + sy * sy) / (pw * pw);
             }
         }
 
         // ---- Packet_Selection (OFDM.c:685-771): crossing idx[j] is a front iff idx[j] - idx[j-1] > 300
         // (idx[-1] = -1).  Fronts are > 300 apart and a chunk is < 300 positions, so only a lane's
         // first crossing can be one, and its predecessor is the last crossing of the earlier chunks:
-        // an exclusive prefix max over lanes.  The first front x with a later front and
+        // an exclusive prefix max over the block's lanes.  The first front x with a later front and
         // M[front+230] > 0.75 gives packet_idx = front + len_RRC_rx + 1; otherwise 0 (OFDM.c:752-761). ----
         int pm = last;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
-            const int t = __shfl_up(pm, o, 64);
-            if (lane >= o) pm = max(pm, t);
+            const int t2 = __shfl_up(pm, o, 64);
+            if (lane >= o) pm = max(pm, t2);
         }
         int prev = __shfl_up(pm, 1, 64);
         if (lane == 0) prev = -1;
+        if (lane == 63) redi[2 + (tid >> 6)] = pm;  // wave 0's last crossing -> wave 1's prefix
+        __syncthreads();                            // crossing words and wave prefixes are in LDS
+        if (tid >= 64) prev = max(prev, redi[2]);
         const int front = (first >= 0 && first - prev > 300) ? first : -1;
-        __syncthreads();                            // every crossing word is in LDS
         FR_STAMP(1);                                           // packet detection
         const bool valid = front >= 0 && front + 230 < Lc && bit_at(cross, front + 230);
-        const int maxf = wave_max_i(front);
-        const int cand = wave_min_i((valid && front < maxf) ? front : 0x7fffffff);
+        const int maxf = block_max_i(front, redi);
+        const int cand = block_min_i((valid && front < maxf) ? front : 0x7fffffff, redi);
         const bool sync_fail = cand == 0x7fffffff;
         const int p = sync_fail ? 0 : cand + 10 + 1;           // len_RRC_rx + 1 (OFDM.c:758)
         FR_STAMP(2);                                           // packet selection
 
-        // ---- RRC matched filter at the down-sampled instants p + 2i (OFDM.c:965, 992-996): a lane
-        // takes 8 consecutive outputs, i.e. one 35-sample window of the capture held in registers ----
+        // ---- RRC matched filter at the down-sampled instants p + 2i (OFDM.c:965, 992-996): outputs
+        // interleaved over the lanes, so a tap's reads are 2 samples apart across lanes (no bank
+        // conflicts); clamped reads + select are Convolution's zero padding ----
         bool oob_l = false;
-        for (int ib = 8 * lane; ib < nfr; ib += 512) {
-            const int nb = p + 2 * ib - 20;             // first capture sample the 8 outputs touch
-            float2 win[35];
+        for (int ii = tid; ii < nfr; ii += SYNC_THREADS) {
+            const int n = p + 2 * ii;
+            float2 v = make_float2(0.f, 0.f);
+            if (n >= 20 && n < L) {                              // interior: all 21 taps inside
 #pragma unroll
-            for (int k = 0; k < 35; ++k) {
-                const int m = nb + k;
-                win[k] = (m >= 0 && m < L) ? r[m] : make_float2(0.f, 0.f);   // Convolution zero-pads
-            }
-#pragma unroll
-            for (int t = 0; t < 8; ++t) {
-                const int i = ib + t;
-                if (i >= nfr) break;
-                float2 v = make_float2(0.f, 0.f);
-                if (p + 2 * i >= L + 20) {
-                    oob_l = true;                                // the reference reads past its buffer
-                } else {
-#pragma unroll
-                    for (int j = 0; j < 21; ++j) {
-                        const float2 x = win[2 * t + 20 - j];
-                        v.x = fmaf(x.x, a.taps[j], v.x);
-                        v.y = fmaf(x.y, a.taps[j], v.y);
-                    }
+                for (int j = 0; j < 21; ++j) {
+                    const float2 x = r[n - j];
+                    v.x = fmaf(x.x, a.taps[j], v.x);
+                    v.y = fmaf(x.y, a.taps[j], v.y);
                 }
-                fr[i] = v;
+            } else if (n >= L + 20) {
+                oob_l = true;                                    // the reference reads past its buffer
+            } else {
+#pragma unroll
+                for (int j = 0; j < 21; ++j) {
+                    const int m = n - j;
+                    float2 x = r[min(max(m, 0), L - 1)];
+                    x = (m >= 0 && m < L) ? x : make_float2(0.f, 0.f);
+                    v.x = fmaf(x.x, a.taps[j], v.x);
+                    v.y = fmaf(x.y, a.taps[j], v.y);
+                }
             }
+            fr[ii] = v;
         }
-        const bool oob = __any(oob_l);
-        __syncthreads();
+        const bool oob = block_max_i(oob_l ? 1 : 0, redi) != 0;   // also orders fr[] for every lane
         FR_STAMP(3);                                           // matched filter + down-sample
 
         // ---- Coarse CFO (OFDM.c:773-804): 16-lag autocorrelation of the short preamble ----
         float px = 0.f, py = 0.f;
-        if (lane < 16) { const float2 u = fr[80 + lane], v = fr[96 + lane]; px = u.x * v.x + u.y * v.y; py = u.y * v.x - u.x * v.y; }
-        px = wave_sum_f(px); py = wave_sum_f(py);
+        if (tid < 16) { const float2 u = fr[80 + tid], v = fr[96 + tid]; px = u.x * v.x + u.y * v.y; py = u.y * v.x - u.x * v.y; }
+        px = block_sum_f(px, redf); py = block_sum_f(py, redf);
         double fc = (-1.0 / (2.0 * M_PI * 16.0 * TS)) * (double)atan2f(py, px);
         if (a.float_cfo) fc = (double)(float)fc;
-        for (int i = lane; i < nfr; i += 64) fr[i] = cfo_rot(fr[i], fc * TS, i);
+        for (int k = tid; k < nfr; k += SYNC_THREADS) fr[k] = cfo_rot(fr[k], fc * TS, k);
         __syncthreads();
         // ---- Fine CFO (OFDM.c:806-828): 64-lag over the two long training symbols ----
-        {
-            const float2 u = fr[192 + lane], v = fr[256 + lane];
-            px = wave_sum_f(u.x * v.x + u.y * v.y);
-            py = wave_sum_f(u.y * v.x - u.x * v.y);
+        px = 0.f; py = 0.f;
+        if (tid < 64) {
+            const float2 u = fr[192 + tid], v = fr[256 + tid];
+            px = u.x * v.x + u.y * v.y;
+            py = u.y * v.x - u.x * v.y;
         }
+        px = block_sum_f(px, redf); py = block_sum_f(py, redf);
         double ff = (-1.0 / (2.0 * M_PI * 64.0 * TS)) * (double)atan2f(py, px);
         if (a.float_cfo) ff = (double)(float)ff;
+        for (int k = tid; k < nfr; k += SYNC_THREADS) fr[k] = cfo_rot(fr[k], ff * TS, k);
         __syncthreads();
-        for (int i = lane; i < nfr; i += 64) fr[i] = cfo_rot(fr[i], ff * TS, i);
-        __syncthreads();
-        if (a.dbg_frame && it == 0) for (int i = lane; i < nfr; i += 64) a.dbg_frame[i] = fr[i];
+        if (a.dbg_frame && first_item) for (int k = tid; k < nfr; k += SYNC_THREADS) a.dbg_frame[k] = fr[k];
         FR_STAMP(4);                                           // coarse + fine CFO
 
-        // ---- LS estimate + CP strip + fft + ZF + slicer + demap (OFDM.c:830-1100).  Quad k carries
-        // {LTF1, LTF2, D_2k, D_2k+1}: the estimate is formed inside each quad (two broadcasts) ----
-        const int role = lane & 3;
-        const int dsym = 2 * (lane >> 2) + (role & 1);
-        const bool dlane = role >= 2 && dsym < a.n_data;
-        const int dsc = min(dsym, a.n_data - 1);
-        const int w0 = role == 0 ? 192 : role == 1 ? 256 : 336 + 80 * dsc;
-        float2 x[64];
-        static_for<0, 64>([&](auto nc) {
-            constexpr int n = decltype(nc)::value;
-            const float2 v = fr[w0 + n];
-            x[n] = (n & 1) ? make_float2(-v.x, -v.y) : v;        // fft() = DFT(x (-1)^n)
-        });
-#ifndef OFDM_FRAME_NO_FFT   // profiling switch: time the sync phases alone
-        fft64<false>(x);
-#endif
-        const uint32_t w[3] = {a.table[3 * dsc], a.table[3 * dsc + 1], a.table[3 * dsc + 2]};
-        SymState st;
-        sym_init(st);
-        const bool dump = a.dbg_eq && it == 0 && dlane;
-        float2 *deq = dump ? a.dbg_eq + 48 * dsym : nullptr;
-        auto Hof = [&](float2 Y, auto binc) { return ls_equalise<decltype(binc)::value>(Y); };
-#ifndef OFDM_FRAME_NO_FFT
-        static_for<0, 4>([&](auto rc) { demap_sub<true, decltype(rc)::value, 2>(x, w, Hof, deq, st); });
-#else
-        st.evm_pre = x[5].x;
-#endif
-        FR_STAMP(5);                                           // FFT + LS + demap
-        const float fe = wave_sum_f(dlane ? finish_evm<2>(st) : 0.f);
-        const uint32_t ferr = wave_sum_u32(dlane ? st.be : 0u), fax = wave_sum_u32(dlane ? st.ax : 0u);
-        if (lane == 0) {
-            unsigned long long *sl = s.acc + q * ACC_SLOTS;
-            sl[0] += ferr;
-            sl[1] += ferr > 0u;
-            sl[2] += fax;
+        // ---- hand-off: LTF1 [192,256), LTF2 [256,320), data d [336 + 80 d, +64) (OFDM.c:830-850,
+        // 1024-1040), plus the sync outcome ----
+        const int nw = 2 + a.n_data;
+        float2 *dst = a.win + i * (int64_t)(nw * 64);
+        for (int e = tid; e < nw * 64; e += SYNC_THREADS) {
+            const int w = e >> 6, n = e & 63;
+            const int w0 = w == 0 ? 192 : w == 1 ? 256 : 336 + 80 * (w - 2);
+            dst[e] = fr[w0 + n];
+        }
+        if (tid == 0) {
+            a.info[i] = make_int4(p, sync_fail, oob, rx_start);
+            unsigned long long *sl = acc + q * ACC_SLOTS;
             sl[3] += sync_fail;
             sl[4] += oob;
-            const float N = 48.0f * (float)a.n_data;
-            sl[5] += (unsigned long long)(int64_t)__float2ll_rn(fe * (float)OFDM_EVM_Q_SCALE);
-            const float db = fe > 0.f ? fmaxf(3.01029995663981195214f * __builtin_amdgcn_logf(fe / N), -400.f) : -400.f;
-            sl[6] += (unsigned long long)(int64_t)__float2ll_rn(db * (float)OFDM_EVM_Q_SCALE);
-            float dbp = -INFINITY;
-            if (fax > 0u) {
-                dbp = 3.01029995663981195214f * __builtin_amdgcn_logf(2.0f * (float)fax / N);
-                sl[7] += (unsigned long long)(int64_t)__float2ll_rn(dbp * (float)OFDM_EVM_Q_SCALE);
-                sl[8] += 1ull;
-            }
             if (a.pidx_out) a.pidx_out[(int64_t)q * a.n_trials + ti] = p;
-            if (it == 0) {
-                if (a.dbg_res) { a.dbg_res[0] = db; a.dbg_res[1] = dbp; a.dbg_res[2] = (float)ferr / (96.0f * a.n_data); }
-                if (a.dbg_ints) { a.dbg_ints[0] = p; a.dbg_ints[1] = sync_fail; a.dbg_ints[2] = oob; a.dbg_ints[3] = rx_start; }
-            }
-        }
-        if (it == 0 && a.dbg_bits && dlane) {
-            a.dbg_bits[3 * dsym] = st.d[0]; a.dbg_bits[3 * dsym + 1] = st.d[1]; a.dbg_bits[3 * dsym + 2] = st.d[2];
+            if (first_item && a.dbg_ints) { a.dbg_ints[0] = p; a.dbg_ints[1] = sync_fail; a.dbg_ints[2] = oob; a.dbg_ints[3] = rx_start; }
         }
         __syncthreads();
-        FR_STAMP(6);                                           // counters
+        FR_STAMP(6);                                           // hand-off
     }
 #ifdef OFDM_FRAME_STAMPS
     if (threadIdx.x == 0 && a.stamps)
         for (int k = 0; k < 7; ++k) atomicAdd(&a.stamps[k], stamp_acc[k]);
 #endif
     __syncthreads();
-    for (int i = lane; i < a.n_snr * 9; i += 64) {
-        const int q = i / 9, k = i % 9;
-        const unsigned long long v = s.acc[q * ACC_SLOTS + k];
-        if (!v) continue;
-        const int c = k == 0 ? OFDM_C_BIT_ERR : k == 1 ? OFDM_C_FRAME_ERR : k == 2 ? OFDM_C_EVM_POST_AXIS
-                    : k == 3 ? OFDM_C_SYNC_FAIL : k == 4 ? OFDM_C_OOB : k == 5 ? OFDM_C_EVM_PRE_Q
-                    : k == 6 ? OFDM_C_EVMDB_PRE_Q : k == 7 ? OFDM_C_EVMDB_POST_Q : OFDM_C_EVMDB_POST_FINITE;
-        atomicAdd(&a.counters[q * OFDM_NCOUNTERS + c], v);
-    }
-    if (a.word_stats) {
-        for (int q = lane; q < a.n_snr; q += 64) {
-            long long *c = reinterpret_cast<long long *>(a.counters + q * OFDM_NCOUNTERS);
-            atomicMin(&c[OFDM_C_WL_MIN_Q], (long long)s.acc[q * ACC_SLOTS + 10]);
-            atomicMax(&c[OFDM_C_WL_MAX_Q], (long long)s.acc[q * ACC_SLOTS + 11]);
+    for (int k = tid; k < a.n_snr; k += SYNC_THREADS) {
+        unsigned long long *c = a.counters + k * OFDM_NCOUNTERS;
+        const unsigned long long *sl = acc + k * ACC_SLOTS;
+        if (sl[3]) atomicAdd(&c[OFDM_C_SYNC_FAIL], sl[3]);
+        if (sl[4]) atomicAdd(&c[OFDM_C_OOB], sl[4]);
+        if (a.word_stats) {
+            atomicMin(reinterpret_cast<long long *>(&c[OFDM_C_WL_MIN_Q]), (long long)sl[10]);
+            atomicMax(reinterpret_cast<long long *>(&c[OFDM_C_WL_MAX_Q]), (long long)sl[11]);
         }
     }
-    if (blockIdx.x == 0) {
-        for (int q = lane; q < a.n_snr; q += 64) {
+}
+
+// ---------------------------------------------------------------- K4b': symbols of the synced frames
+// LS estimate + CP strip + fft + ZF + slicer + demap (OFDM.c:830-1165) for a batch of items: a quad
+// carries {LTF1, LTF2, D_2k, D_2k+1} of one item (estimate formed inside the quad with two DPP
+// broadcasts), ceil(n_data / 2) quads per item, 16 quads per wave.
+constexpr int SYM_THREADS = 256;
+template <bool DUMP>   // DUMP: item 0's bits / subcarriers / metrics for ofdm_receiver
+__global__ __launch_bounds__(SYM_THREADS, 2) void frame_sym_kernel(FrameArgs a) {
+    __shared__ unsigned long long acc[OFDM_MAX_SNR][8];
+    __shared__ float part_e[SYM_THREADS / 4][2];             // per quad: EVM of its two data symbols
+    __shared__ uint32_t part_b[SYM_THREADS / 4][2], part_a[SYM_THREADS / 4][2];
+    for (int k = threadIdx.x; k < a.n_snr * 8; k += SYM_THREADS) (&acc[0][0])[k] = 0ull;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, quad = threadIdx.x >> 2, role = lane & 3;
+    const int qpi = (a.n_data + 1) / 2, ipb = (SYM_THREADS / 4) / qpi;   // quads per item, items per block
+    const int item_l = quad / qpi, qi = quad - item_l * qpi;
+    const int dsym = 2 * qi + (role & 1);
+    const int nw = 2 + a.n_data;
+    const int dsc = min(dsym, a.n_data - 1);
+    const int w = role < 2 ? role : 2 + dsc;
+    for (int64_t base = (int64_t)blockIdx.x * ipb; base < a.n_items; base += (int64_t)gridDim.x * ipb) {
+        const int64_t i = base + item_l;
+        const bool item_ok = item_l < ipb && i < a.n_items;
+        const bool dlane = item_ok && role >= 2 && dsym < a.n_data;
+        const float2 *src = a.win + (item_ok ? i : 0) * (int64_t)(nw * 64) + w * 64;
+        float2 x[64];
+        // load fused with the first radix-4 stage, 16 samples at a time (fft() = DFT(x (-1)^n))
+        static_for<0, 4>([&](auto gc) {
+            constexpr int g = decltype(gc)::value;
+            gcf2 *sp = (gcf2 *)src;
+            opaque(sp);
+            static_for<0, 16>([&](auto pc) {
+                constexpr int n = 16 * (decltype(pc)::value >> 2) + 4 * g + (decltype(pc)::value & 3);
+                const float2 v = gld(sp, n);
+                x[n] = (n & 1) ? make_float2(-v.x, -v.y) : v;
+            });
+            static_for<0, 4>([&](auto ic) { dif_stage1<false, 4 * g + decltype(ic)::value>(x); });
+            sched_fence();
+        });
+        const uint32_t wd[3] = {a.table[3 * dsc], a.table[3 * dsc + 1], a.table[3 * dsc + 2]};
+        SymState st;
+        sym_init(st);
+        const bool dump = DUMP && a.dbg_eq && item_ok && a.item0 + i == 0 && dlane;
+        float2 *deq = dump ? a.dbg_eq + 48 * dsym : nullptr;
+        auto Hof = [&](float2 Y, auto binc) { return ls_equalise<decltype(binc)::value>(Y); };
+        static_for<0, 4>([&](auto rc) {
+            constexpr int R = decltype(rc)::value;
+            dif_sub16<false, R>(x);
+            demap_sub<DUMP, R, 2>(x, wd, Hof, deq, st);
+            sched_fence();
+        });
+        if (role >= 2) {
+            part_e[quad][role & 1] = dlane ? finish_evm<2>(st) : 0.f;
+            part_b[quad][role & 1] = dlane ? st.be : 0u;
+            part_a[quad][role & 1] = dlane ? st.ax : 0u;
+        }
+        if (DUMP && dump && a.dbg_bits) { a.dbg_bits[3 * dsym] = st.d[0]; a.dbg_bits[3 * dsym + 1] = st.d[1]; a.dbg_bits[3 * dsym + 2] = st.d[2]; }
+        __syncthreads();
+        if (item_ok && qi == 0 && role == 0) {
+            // the item's totals in symbol order (deterministic), then the trial's metrics
+            float fe = 0.f;
+            uint32_t ferr = 0u, fax = 0u;
+            for (int k = 0; k < qpi; ++k)
+                for (int r2 = 0; r2 < 2; ++r2) {
+                    fe += part_e[quad + k][r2]; ferr += part_b[quad + k][r2]; fax += part_a[quad + k][r2];
+                }
+            const int64_t g = a.item0 + i;
+            const int q = (int)(g % a.n_snr);
+            unsigned long long *sl = acc[q];
+            atomicAdd(&sl[0], (unsigned long long)ferr);
+            atomicAdd(&sl[1], (unsigned long long)(ferr > 0u));
+            atomicAdd(&sl[2], (unsigned long long)fax);
+            const float N = 48.0f * (float)a.n_data;
+            atomicAdd(&sl[5], (unsigned long long)(int64_t)__float2ll_rn(fe * (float)OFDM_EVM_Q_SCALE));
+            const float db = fe > 0.f ? fmaxf(3.01029995663981195214f * __builtin_amdgcn_logf(fe / N), -400.f) : -400.f;
+            atomicAdd(&sl[6], (unsigned long long)(int64_t)__float2ll_rn(db * (float)OFDM_EVM_Q_SCALE));
+            float dbp = -INFINITY;
+            if (fax > 0u) {
+                dbp = 3.01029995663981195214f * __builtin_amdgcn_logf(2.0f * (float)fax / N);
+                atomicAdd(&sl[7], (unsigned long long)(int64_t)__float2ll_rn(dbp * (float)OFDM_EVM_Q_SCALE));
+                atomicAdd(&sl[4], 1ull);
+            }
+            if (DUMP && g == 0 && a.dbg_res) { a.dbg_res[0] = db; a.dbg_res[1] = dbp; a.dbg_res[2] = (float)ferr / (96.0f * a.n_data); }
+        }
+        __syncthreads();
+    }
+    for (int k = threadIdx.x; k < a.n_snr * 6; k += SYM_THREADS) {
+        const int q = k / 6, s2 = k % 6;
+        const int slot = s2 < 3 ? s2 : s2 + 1;           // 0 bit_err, 1 frame_err, 2 axis, 4 finite, 5 pre, 6 dbpre, 7 dbpost
+        const unsigned long long v = acc[q][slot];
+        if (!v) continue;
+        const int c = slot == 0 ? OFDM_C_BIT_ERR : slot == 1 ? OFDM_C_FRAME_ERR : slot == 2 ? OFDM_C_EVM_POST_AXIS
+                    : slot == 4 ? OFDM_C_EVMDB_POST_FINITE : slot == 5 ? OFDM_C_EVM_PRE_Q : OFDM_C_EVMDB_PRE_Q;
+        atomicAdd(&a.counters[q * OFDM_NCOUNTERS + c], v);
+    }
+    for (int q = threadIdx.x; q < a.n_snr; q += SYM_THREADS)
+        if (acc[q][7]) atomicAdd(&a.counters[q * OFDM_NCOUNTERS + OFDM_C_EVMDB_POST_Q], acc[q][7]);
+    if (blockIdx.x == 0 && a.add_totals) {
+        for (int q = threadIdx.x; q < a.n_snr; q += SYM_THREADS) {
             unsigned long long *c = a.counters + q * OFDM_NCOUNTERS;
             const unsigned long long nt = (unsigned long long)a.n_trials, nd = (unsigned long long)a.n_data;
             atomicAdd(&c[OFDM_C_FRAMES], nt);
@@ -682,13 +780,37 @@ static int32_t word_bits(double mn, double mx) {
     return max_abs < 1.0f ? 1 : (int32_t)std::ceil(std::log2((double)max_abs)) + 1;
 }
 
-static unsigned frame_grid(Ctx *c, int64_t items, size_t lds) {
+static unsigned occupancy_grid(const void *kernel, int threads, size_t lds, int cus, int64_t blocks) {
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(&frame_rx_kernel), 64,
-                                                     lds) != hipSuccess || per_cu < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, lds) != hipSuccess || per_cu < 1)
         per_cu = 2;
-    const int64_t cap = (int64_t)per_cu * c->cus * 4;
-    return (unsigned)std::max<int64_t>(1, std::min(items, cap));
+    return (unsigned)std::max<int64_t>(1, std::min<int64_t>(blocks, (int64_t)per_cu * cus * 2));
+}
+
+constexpr int64_t FRAME_CHUNK_ITEMS = int64_t(1) << 18;   // items per sync -> symbol hand-off (<= 1 GB)
+
+// K4b then K4b' over a.n_items items starting at a.item0, through the context's hand-off buffer
+static int run_frame_chunk(Ctx *c, FrameArgs &a) {
+    const int nw = 2 + a.n_data;
+    const size_t wbytes = (size_t)a.n_items * nw * 64 * sizeof(float2);
+    int rc = c->ensure(&c->d_scratch, &c->cap_scratch, wbytes + (size_t)a.n_items * sizeof(int4) + 256);
+    if (rc) return rc;
+    a.win = (float2 *)c->d_scratch;
+    a.info = (int4 *)((char *)c->d_scratch + ((wbytes + 255) & ~size_t(255)));
+    const size_t lds = frame_lds_bytes(a.cap_len, a.n_data, a.n_snr);
+    hipLaunchKernelGGL(frame_sync_kernel,
+                       dim3(occupancy_grid(reinterpret_cast<const void *>(&frame_sync_kernel), SYNC_THREADS, lds,
+                                           c->cus, a.n_items)),
+                       dim3(SYNC_THREADS), lds, c->stream, a);
+    const int ipb = (SYM_THREADS / 4) / ((a.n_data + 1) / 2);
+    const bool dump = a.dbg_eq || a.dbg_bits || a.dbg_res;
+    const void *k = dump ? reinterpret_cast<const void *>(&frame_sym_kernel<true>)
+                         : reinterpret_cast<const void *>(&frame_sym_kernel<false>);
+    const dim3 grid(occupancy_grid(k, SYM_THREADS, 0, c->cus, (a.n_items + ipb - 1) / ipb));
+    if (dump) hipLaunchKernelGGL(frame_sym_kernel<true>, grid, dim3(SYM_THREADS), 0, c->stream, a);
+    else hipLaunchKernelGGL(frame_sym_kernel<false>, grid, dim3(SYM_THREADS), 0, c->stream, a);
+    HIPOK(hipGetLastError());
+    return OFDM_OK;
 }
 
 extern "C" {
@@ -759,11 +881,13 @@ int ofdm_receiver(ofdm_ctx *ctx, const float *capture, const ofdm_rx_opts *opts,
     a.dbg_ints = (int32_t *)(base + off_int);
     a.dbg_bits = (uint32_t *)(base + off_bits);
     a.dbg_eq = (float2 *)(base + off_eq);
-    const size_t lds = frame_lds_bytes(L, nd, 1);
+    a.item0 = 0;
+    a.n_items = 1;
+    a.add_totals = 1;
     c->tic(Ctx::K_FRAME);
-    hipLaunchKernelGGL(frame_rx_kernel, dim3(1), dim3(64), lds, c->stream, a);
+    rc = run_frame_chunk(c, a);
     c->toc();
-    HIPOK(hipGetLastError());
+    if (rc) return rc;
     float res[4];
     int32_t ints[4];
     uint32_t words[3 * FR_MAX_DATA];
@@ -818,23 +942,27 @@ int ofdm_frame_sweep(ofdm_ctx *ctx, const ofdm_cfg *cfg, const ofdm_rx_opts *opt
         for (int q = 0; q < a.n_snr; ++q)   // sigma^2 = P / 10^(snr/10) (OFDM.c:645-647)
             a.sigma[q] = (float)std::sqrt(c->wave_power / std::pow(10.0, snr_db[q0 + q] / 10.0));
         if (n_trials == 0) continue;
-        const size_t lds = frame_lds_bytes(a.cap_len, a.n_data, a.n_snr);
 #ifdef OFDM_FRAME_STAMPS
         unsigned long long *dst = nullptr;
         HIPOK(hipMalloc(&dst, 64));
         HIPOK(hipMemset(dst, 0, 64));
         a.stamps = dst;
 #endif
+        const int64_t items = n_trials * a.n_snr;
         c->tic(Ctx::K_FRAME);
-        hipLaunchKernelGGL(frame_rx_kernel, dim3(frame_grid(c, n_trials * a.n_snr, lds)), dim3(64), lds, c->stream, a);
+        for (int64_t i0 = 0; i0 < items; i0 += FRAME_CHUNK_ITEMS) {
+            a.item0 = i0;
+            a.n_items = std::min(FRAME_CHUNK_ITEMS, items - i0);
+            a.add_totals = i0 + a.n_items >= items;
+            if ((rc = run_frame_chunk(c, a))) { c->toc(); return rc; }
+        }
         c->toc();
-        HIPOK(hipGetLastError());
 #ifdef OFDM_FRAME_STAMPS
         unsigned long long hs[8];
         HIPOK(hipMemcpy(hs, dst, 64, hipMemcpyDeviceToHost));
         hipFree(dst);
-        static const char *names[7] = {"capture+noise", "detection", "selection", "matched filter", "cfo",
-                                       "fft+ls+demap", "counters"};
+        static const char *names[7] = {"capture+noise", "detection", "selection", "matched filter", "cfo", "-",
+                                       "hand-off"};
         double tot = 0;
         for (int k = 0; k < 7; ++k) tot += (double)hs[k];
         for (int k = 0; k < 7; ++k)
