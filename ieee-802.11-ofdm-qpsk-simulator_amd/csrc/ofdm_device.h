@@ -59,6 +59,32 @@ __device__ __forceinline__ uint4 philox10(uint32_t c0, uint32_t c1, uint32_t c2,
     return make_uint4(c0, c1, c2, c3);
 }
 
+// philox10 for many calls that share counter words c0, c1 (the frame) and c3 (stream | SNR index)
+// and differ only in c2: round 1's c0 product does not depend on c2, so philox_head() computes it
+// once and philox10_c2() does the c2 half of round 1 and rounds 2..10 (same output as philox10).
+struct PhiloxHead { uint32_t c1, n2, c3; };
+__device__ __forceinline__ PhiloxHead philox_head(uint32_t c0, uint32_t c1, uint32_t c3, uint32_t k1) {
+    const uint64_t p0 = (uint64_t)PHILOX_M0 * c0;
+    return {c1, (uint32_t)__builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c3, k1, 0x96), (uint32_t)p0};
+}
+__device__ __forceinline__ uint4 philox10_c2(const PhiloxHead &h, uint32_t c2, uint32_t k0, uint32_t k1) {
+    const uint64_t p1r = (uint64_t)PHILOX_M1 * c2;
+    uint32_t c0 = __builtin_amdgcn_bitop3_b32((uint32_t)(p1r >> 32), h.c1, k0, 0x96);
+    uint32_t c1 = (uint32_t)p1r, c3 = h.c3;
+    c2 = h.n2;
+    k0 += PHILOX_W0; k1 += PHILOX_W1;
+#pragma unroll
+    for (int r = 1; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)PHILOX_M0 * c0;
+        const uint64_t p1 = (uint64_t)PHILOX_M1 * c2;
+        const uint32_t n0 = __builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c1, k0, 0x96);
+        const uint32_t n2 = __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c3, k1, 0x96);
+        c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
+        k0 += PHILOX_W0; k1 += PHILOX_W1;
+    }
+    return make_uint4(c0, c1, c2, c3);
+}
+
 // Box-Muller pair.  u1 = fma((float)x1, 2^-32, 2^-33) in (0, 1] (tail to 6.7 sigma);
 // u2 = (float)x2 * 2^-32 in revolutions.  Same quantisation as oracle/ofdm_oracle.c:bm_pair.
 __device__ __forceinline__ float2 box_muller(uint32_t x1, uint32_t x2) {
@@ -77,18 +103,18 @@ __device__ __forceinline__ float noise_k(float sigma) { return -1.38629436111989
 
 // four N(0,1) draws of one Philox block
 struct Gauss4 { float z[4]; };
-__device__ __forceinline__ Gauss4 gauss4(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
-                                         uint32_t k0, uint32_t k1) {
-    const uint4 o = philox10(c0, c1, c2, c3, k0, k1);
+__device__ __forceinline__ Gauss4 gauss4_of(uint4 o) {
     const float2 a = box_muller(o.x, o.y), b = box_muller(o.z, o.w);
     Gauss4 g;
     g.z[0] = a.x; g.z[1] = a.y; g.z[2] = b.x; g.z[3] = b.y;
     return g;
 }
+__device__ __forceinline__ Gauss4 gauss4(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                         uint32_t k0, uint32_t k1) {
+    return gauss4_of(philox10(c0, c1, c2, c3, k0, k1));
+}
 
-__device__ __forceinline__ Noise4 noise4(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
-                                         float K) {
-    const uint4 o = philox10(c0, c1, c2, c3, k0, k1);
+__device__ __forceinline__ Noise4 noise4_of(uint4 o, float K) {
     const float u1a = fmaf((float)o.x, 0x1p-32f, 0x1p-33f), u2a = (float)o.y * 0x1p-32f;
     const float u1b = fmaf((float)o.z, 0x1p-32f, 0x1p-33f), u2b = (float)o.w * 0x1p-32f;
     Noise4 n;

@@ -347,6 +347,7 @@ __global__ __launch_bounds__(SYNC_THREADS) void frame_sync_kernel(FrameArgs a) {
             for (int n = tid; n < L; n += SYNC_THREADS) r[n] = a.ext[n];
         } else {
             const int b0 = rx_start >> 2, b1 = (rx_start + L - 1) >> 2;
+            const PhiloxHead hd = philox_head(t_lo, t_hi, STREAM_NOISE | qs, a.k1);   // shared by all blocks
             // Gaussian k of the trial's stream goes to waveform sample k (as if Transmission_Over_Air
             // had drawn the whole waveform); only the captured samples are ever evaluated.  Four
             // Philox blocks per lane per pass, their waveform loads issued first.
@@ -364,7 +365,7 @@ __global__ __launch_bounds__(SYNC_THREADS) void frame_sync_kernel(FrameArgs a) {
                     const int b = bb + SYNC_THREADS * u;
                     if (b > b1) break;
                     Gauss4 gz;
-                    if (a.noise == OFDM_NOISE_REAL) gz = gauss4(t_lo, t_hi, (uint32_t)b, STREAM_NOISE | qs, a.k0, a.k1);
+                    if (a.noise == OFDM_NOISE_REAL) gz = gauss4_of(philox10_c2(hd, (uint32_t)b, a.k0, a.k1));
                     float2 w[4];
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {

@@ -51,6 +51,7 @@ struct RxArgs {
     float2 *dump_eq;                   // optional parity dumps
     uint32_t *dump_bits;
     int64_t dump_frames;               // leading dimension of the dumps (frames)
+    unsigned long long *stamps;        // OFDM_RX_STAMPS builds: cycles per receiver phase [5]
     float sigma[OFDM_MAX_SNR];
 };
 

@@ -148,61 +148,73 @@ struct EqFn {
 template <typename F>
 __device__ __forceinline__ EqFn<F> eq_fn(F f) { return EqFn<F>{f}; }
 
-// frame-level counters of one wave, reduced and added into the block's LDS slots
+// Frame-level counters of one frame's leader lane.  They go straight into the block's LDS slots,
+// one ds_add_u64 per lane and slot (the LDS pipe serialises the lanes; no VALU wave reduction).
+// Slots of sacc[q]:
+//   0: bit errors | slicer axis errors << 32      1: frame errors | finite post-slicer EVM_dB << 32
+//   2: EVM_PRE_Q      3: EVMDB_PRE_Q      4: EVMDB_POST_Q
+// A 32-bit field cannot carry into its neighbour: one launch covers at most MAX_BATCH_FRAMES = 2^23
+// frames, and 2^23 x 192 < 2^32.
 struct FrameAcc {
-    uint32_t bit_err = 0, frame_err = 0, axis = 0, post_finite = 0;
+    uint64_t errs = 0, frames = 0;     // packed slots 0 and 1
     int64_t pre_q = 0, dbpre_q = 0, dbpost_q = 0;
 };
 
+// x 2^20 rounded to nearest even, as the oracle's q20(): x >= 0 (a frame's sum |z - d|^2)
+__device__ __forceinline__ int64_t q20_nonneg(float x) {
+    const float v = __builtin_rintf(x * (float)OFDM_EVM_Q_SCALE);      // integer-valued
+    const float hi = __builtin_floorf(v * 0x1p-32f);
+    const uint32_t lo = (uint32_t)fmaf(hi, -0x1p32f, v);                 // exact: 0 <= v - hi 2^32 < 2^32
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | lo);
+}
+// |x| 2^20 < 2^31: a frame's EVM_dB (floor -400 dB; 10 log10(FLT_MAX / 96) < 366 dB)
+__device__ __forceinline__ int64_t q20_db(float db) {
+    return (int64_t)(int32_t)__builtin_rintf(db * (float)OFDM_EVM_Q_SCALE);
+}
+
 __device__ __forceinline__ void frame_metrics(FrameAcc &acc, float fe_pre, uint32_t ferr, uint32_t fax) {
-    const float N = 96.0f;   // 48 subcarriers x D = 2
-    acc.bit_err += ferr;
-    acc.frame_err += ferr > 0u;
-    acc.axis += fax;
-    acc.pre_q += (int64_t)__float2ll_rn(fe_pre * (float)OFDM_EVM_Q_SCALE);
-    // per-frame EVM_dB = 10 log10(sum|e|^2 / sum|d|^2), |d| = 1 (OFDM.c:1124-1126), floor -400 dB
-    const float lg = 3.01029995663981195214f * __builtin_amdgcn_logf(fe_pre / N);   // 10 log10(2) log2
-    const float db = fe_pre > 0.f ? fmaxf(lg, -400.0f) : -400.0f;
-    acc.dbpre_q += (int64_t)__float2ll_rn(db * (float)OFDM_EVM_Q_SCALE);
-    if (fax > 0u) {
-        const float dbp = 3.01029995663981195214f * __builtin_amdgcn_logf(2.0f * (float)fax / N);
-        acc.dbpost_q += (int64_t)__float2ll_rn(dbp * (float)OFDM_EVM_Q_SCALE);
-        acc.post_finite += 1u;
+    // per-frame EVM_dB = 10 log10(sum|e|^2 / N), N = 96 terms (48 subcarriers x D = 2, OFDM.c:1124-1126),
+    // as 10 log10(2) (log2(sum) - log2 96); floor -400 dB.  After the slicer sum|s - d|^2 = 2 fax
+    // (OFDM.c:1128-1150): 10 log10(2 fax / 96).
+    constexpr float K = 3.01029995663981195214f, L96 = 6.58496250072115618146f;
+    acc.errs = (uint64_t)ferr | ((uint64_t)fax << 32);
+    acc.frames = (uint64_t)(ferr > 0u) | ((uint64_t)(fax > 0u) << 32);
+    acc.pre_q = q20_nonneg(fe_pre);
+    const float lg = K * (__builtin_amdgcn_logf(fe_pre) - L96);
+    acc.dbpre_q = q20_db(fe_pre > 0.f ? fmaxf(lg, -400.0f) : -400.0f);
+    acc.dbpost_q = fax > 0u ? q20_db(K * (__builtin_amdgcn_logf((float)fax) + (1.0f - L96))) : 0;
+}
+
+__device__ __forceinline__ void flush_lanes(const FrameAcc &acc, bool leader, unsigned long long *slots /*[8]*/) {
+    if (leader) {
+        atomicAdd(&slots[0], (unsigned long long)acc.errs);
+        atomicAdd(&slots[1], (unsigned long long)acc.frames);
+        atomicAdd(&slots[2], (unsigned long long)acc.pre_q);
+        atomicAdd(&slots[3], (unsigned long long)acc.dbpre_q);
+        atomicAdd(&slots[4], (unsigned long long)acc.dbpost_q);
     }
 }
 
-
-__device__ __forceinline__ void flush_wave(const FrameAcc &acc, unsigned long long *slots /*[8]*/) {
-    // per wave and SNR: bit_err, axis <= 32 frames x 192 < 2^16; frame counts <= 32
-    const uint32_t p0 = wave_sum_u32(acc.bit_err | (acc.axis << 16));
-    const uint32_t p1 = wave_sum_u32(acc.frame_err | (acc.post_finite << 16));
-    const uint32_t a0 = p0 & 0xFFFFu, a2 = p0 >> 16, a1 = p1 & 0xFFFFu, a3 = p1 >> 16;
-    const uint64_t b0 = wave_sum_u64((uint64_t)acc.pre_q), b1 = wave_sum_u64((uint64_t)acc.dbpre_q);
-    const uint64_t b2 = wave_sum_u64((uint64_t)acc.dbpost_q);
-    if ((threadIdx.x & 63) == 0) {
-        atomicAdd(&slots[0], (unsigned long long)a0);
-        atomicAdd(&slots[1], (unsigned long long)a1);
-        atomicAdd(&slots[2], (unsigned long long)a2);
-        atomicAdd(&slots[3], (unsigned long long)a3);
-        atomicAdd(&slots[4], (unsigned long long)b0);
-        atomicAdd(&slots[5], (unsigned long long)b1);
-        atomicAdd(&slots[6], (unsigned long long)b2);
+// term k of an SNR point's LDS slots -> (counter index, value)
+__device__ __forceinline__ int slot_term(const unsigned long long *s, int k, unsigned long long &v) {
+    switch (k) {
+        case 0: v = s[0] & 0xffffffffull; return OFDM_C_BIT_ERR;
+        case 1: v = s[0] >> 32; return OFDM_C_EVM_POST_AXIS;
+        case 2: v = s[1] & 0xffffffffull; return OFDM_C_FRAME_ERR;
+        case 3: v = s[1] >> 32; return OFDM_C_EVMDB_POST_FINITE;
+        case 4: v = s[2]; return OFDM_C_EVM_PRE_Q;
+        case 5: v = s[3]; return OFDM_C_EVMDB_PRE_Q;
+        default: v = s[4]; return OFDM_C_EVMDB_POST_Q;
     }
-}
-
-// LDS slot k -> counter index
-__device__ __forceinline__ int slot_counter(int k) {
-    return k == 0 ? OFDM_C_BIT_ERR : k == 1 ? OFDM_C_FRAME_ERR : k == 2 ? OFDM_C_EVM_POST_AXIS
-         : k == 3 ? OFDM_C_EVMDB_POST_FINITE : k == 4 ? OFDM_C_EVM_PRE_Q : k == 5 ? OFDM_C_EVMDB_PRE_Q
-         : OFDM_C_EVMDB_POST_Q;
 }
 
 __device__ __forceinline__ void block_flush(const RxArgs &a, unsigned long long (*sacc)[8]) {
     __syncthreads();
     for (int i = threadIdx.x; i < a.n_snr * 7; i += blockDim.x) {
         const int q = i / 7, k = i % 7;
-        const unsigned long long v = sacc[q][k];
-        if (v) atomicAdd(&a.counters[q * OFDM_NCOUNTERS + slot_counter(k)], v);
+        unsigned long long v;
+        const int ci = slot_term(sacc[q], k, v);
+        if (v) atomicAdd(&a.counters[q * OFDM_NCOUNTERS + ci], v);
     }
     if (blockIdx.x == 0) {
         for (int q = threadIdx.x; q < a.n_snr; q += blockDim.x) {

@@ -11,6 +11,7 @@
 // noise) four butterflies at a time, then the four 16-point sub-FFTs run one after another and
 // each sub-block's bins are consumed (demapped or stored) at once.  sched_fence() pins that
 // order so the live set stays ~128 VGPRs + temporaries (3 waves/SIMD, no scratch).
+#include <cstdlib>
 #include "ofdm_internal.h"
 #include "ofdm_rxcommon.h"
 
@@ -22,6 +23,36 @@
 #endif
 
 namespace ofdm {
+
+// Diagnostic build (-DOFDM_RX_STAMPS): s_memtime per receiver phase, summed per wave and over the
+// grid.  The stamps' lgkmcnt(0) waits and fences change the schedule: read the phases' SHARES, never
+// this build's run time.  Phases: 0 window + noise + first radix-4 stage, 1 sub-block FFTs,
+// 2 equaliser fetch + demap, 3 frame metrics + counters, 4 group end (wait + barrier).
+#ifdef OFDM_RX_STAMPS
+struct RxStamp {
+    unsigned long long acc[5] = {0, 0, 0, 0, 0};
+    unsigned long long t = 0;
+    __device__ __forceinline__ static unsigned long long now() {
+        unsigned long long v;
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");
+        __builtin_amdgcn_sched_barrier(0);
+        return v;
+    }
+    __device__ __forceinline__ void start() { t = now(); }
+    __device__ __forceinline__ void mark(int k) { const unsigned long long v = now(); acc[k] += v - t; t = v; }
+    __device__ __forceinline__ void flush(unsigned long long *dst) {
+        if (dst && (threadIdx.x & 63) == 0)
+            for (int k = 0; k < 5; ++k) atomicAdd(&dst[k], acc[k]);
+    }
+};
+#else
+struct RxStamp {
+    __device__ __forceinline__ void start() {}
+    __device__ __forceinline__ void mark(int) {}
+    __device__ __forceinline__ void flush(unsigned long long *) {}
+};
+#endif
 
 // ======================================================================== K1: batched FFT
 // One wave = 64 transforms.  Coalesced 16-B loads into a padded LDS image (row = 64 float2 + 1
@@ -182,35 +213,40 @@ __device__ __forceinline__ void stage_group(const RxArgs &a, int64_t col0, float
     }
 }
 
-// Load + channel + AWGN for samples n0..n0+3, times (-1)^n (fft() = DFT of x(-1)^n, OFDM.c:314-318).
-// Noise sample at frame time t uses Gaussian t (real) or 2t, 2t+1 (complex) of the frame's stream
-// (DESIGN.md §3); AWGN is real-only as OFDM.c:651 really does (D7).  K = noise_k(sigma) (real) or
-// noise_k(sigma / sqrt2) (complex): each noisy component is one fma (Noise4).
-template <int NOISE, int CHAN, int N0, typename WS>
-__device__ __forceinline__ void rx_block(float2 (&x)[64], const WS &src, uint32_t f_lo, uint32_t f_hi,
-                                         uint32_t t0, uint32_t q, float K, uint32_t k0, uint32_t k1,
-                                         const float2 (&h)[4]) {
-    // re-materialise per block: keeps LICM from hoisting 16 blocks' worth of addresses / round-1 products
+// Clean samples n0-3..n0+3 (Rayleigh: the 4-tap channel reaches 3 back) or n0..n0+3 of a lane's window.
+template <int CHAN, int N0, typename WS>
+__device__ __forceinline__ void rx_load(float2 (&c)[7], const WS &src) {
+    // re-materialise per block: keeps LICM from hoisting 16 blocks' worth of addresses
     WS p = src;
     p.fresh();
-    uint32_t flo = f_lo, fhi = f_hi, tb = t0;
-    opaque(flo); opaque(fhi); opaque(tb);
-    f_lo = flo; f_hi = fhi; t0 = tb;
-    float nr[8], nt[8];     // noise of component j = nr[j] * nt[j]
-    if constexpr (NOISE == OFDM_NOISE_REAL) {
-        const Noise4 g = noise4(f_lo, f_hi, (t0 >> 2) + (N0 >> 2), STREAM_NOISE | q, k0, k1, K);
-        nr[0] = g.r0; nt[0] = g.c0; nr[1] = g.r0; nt[1] = g.s0; nr[2] = g.r1; nt[2] = g.c1; nr[3] = g.r1; nt[3] = g.s1;
-    } else if constexpr (NOISE == OFDM_NOISE_COMPLEX) {
-        const Noise4 g0 = noise4(f_lo, f_hi, (t0 >> 1) + (N0 >> 1), STREAM_NOISE | q, k0, k1, K);
-        const Noise4 g1 = noise4(f_lo, f_hi, (t0 >> 1) + (N0 >> 1) + 1, STREAM_NOISE | q, k0, k1, K);
-        nr[0] = g0.r0; nt[0] = g0.c0; nr[1] = g0.r0; nt[1] = g0.s0; nr[2] = g0.r1; nt[2] = g0.c1; nr[3] = g0.r1; nt[3] = g0.s1;
-        nr[4] = g1.r0; nt[4] = g1.c0; nr[5] = g1.r0; nt[5] = g1.s0; nr[6] = g1.r1; nt[6] = g1.c1; nr[7] = g1.r1; nt[7] = g1.s1;
-    }
-    float2 c[7];
     if constexpr (CHAN == OFDM_CHAN_RAYLEIGH4) {
         static_for<0, 7>([&](auto ic) { c[decltype(ic)::value] = p.template at<N0 - 3 + decltype(ic)::value>(); });
     } else {
         static_for<0, 4>([&](auto ic) { c[3 + decltype(ic)::value] = p.template at<N0 + decltype(ic)::value>(); });
+    }
+}
+
+// Channel + AWGN for samples n0..n0+3 of loaded clean samples c, times (-1)^n (fft() = DFT of
+// x(-1)^n, OFDM.c:314-318).  Noise sample at frame time t uses Gaussian t (real) or 2t, 2t+1
+// (complex) of the frame's stream; AWGN is real-only as OFDM.c:651 really does (D7).
+// K = noise_k(sigma) (real) or noise_k(sigma / sqrt2) (complex): each noisy component is one fma.
+// `hd` = philox_head of the frame's noise stream at this SNR point; `tb` = the counter word c2 of
+// the window's first Philox block (t0 / 4 real, t0 / 2 complex).
+template <int NOISE, int CHAN, int N0>
+__device__ __forceinline__ void rx_noisy(float2 (&x)[64], const float2 (&c)[7], const PhiloxHead &hd, uint32_t tb,
+                                         float K, uint32_t k0, uint32_t k1, const float2 (&h)[4]) {
+    // re-materialise per block: keeps LICM from hoisting 16 blocks' worth of round-1 products out
+    // of the SNR loop (tb does not depend on the SNR point)
+    opaque(tb);
+    float nr[8], nt[8];     // noise of component j = nr[j] * nt[j]
+    if constexpr (NOISE == OFDM_NOISE_REAL) {
+        const Noise4 g = noise4_of(philox10_c2(hd, tb + (N0 >> 2), k0, k1), K);
+        nr[0] = g.r0; nt[0] = g.c0; nr[1] = g.r0; nt[1] = g.s0; nr[2] = g.r1; nt[2] = g.c1; nr[3] = g.r1; nt[3] = g.s1;
+    } else if constexpr (NOISE == OFDM_NOISE_COMPLEX) {
+        const Noise4 g0 = noise4_of(philox10_c2(hd, tb + (N0 >> 1), k0, k1), K);
+        const Noise4 g1 = noise4_of(philox10_c2(hd, tb + (N0 >> 1) + 1, k0, k1), K);
+        nr[0] = g0.r0; nt[0] = g0.c0; nr[1] = g0.r0; nt[1] = g0.s0; nr[2] = g0.r1; nt[2] = g0.c1; nr[3] = g0.r1; nt[3] = g0.s1;
+        nr[4] = g1.r0; nt[4] = g1.c0; nr[5] = g1.r0; nt[5] = g1.s0; nr[6] = g1.r1; nt[6] = g1.c1; nr[7] = g1.r1; nt[7] = g1.s1;
     }
     static_for<0, 4>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
@@ -230,18 +266,30 @@ __device__ __forceinline__ void rx_block(float2 (&x)[64], const WS &src, uint32_
     });
 }
 
-// generate the window fused with the first radix-4 stage (4 butterflies per group)
+// generate the window fused with the first radix-4 stage (4 butterflies per group of 16 samples).
+// OFDM_RX_EARLY_LOADS pins the group's LDS reads ahead of its noise generation; measured slower
+// (+32 live VGPRs -> more spills; the read latency is already hidden by the other 2 waves/SIMD).
 template <int NOISE, int CHAN, typename WS>
 __device__ __forceinline__ void rx_window_stage1(float2 (&x)[64], const WS &src, uint32_t f_lo,
                                                  uint32_t f_hi, uint32_t t0, uint32_t q, float sigma,
                                                  uint32_t k0, uint32_t k1, const float2 (&h)[4]) {
     const float K = noise_k(NOISE == OFDM_NOISE_COMPLEX ? sigma * INV_SQRT2 : sigma);
+    const PhiloxHead hd = philox_head(f_lo, f_hi, STREAM_NOISE | q, k1);     // shared by the 16-32 blocks
+    const uint32_t tb = NOISE == OFDM_NOISE_COMPLEX ? t0 >> 1 : t0 >> 2;
     static_for<0, 4>([&](auto gc) {
         constexpr int g = decltype(gc)::value;
-        rx_block<NOISE, CHAN, 4 * g>(x, src, f_lo, f_hi, t0, q, K, k0, k1, h);
-        rx_block<NOISE, CHAN, 16 + 4 * g>(x, src, f_lo, f_hi, t0, q, K, k0, k1, h);
-        rx_block<NOISE, CHAN, 32 + 4 * g>(x, src, f_lo, f_hi, t0, q, K, k0, k1, h);
-        rx_block<NOISE, CHAN, 48 + 4 * g>(x, src, f_lo, f_hi, t0, q, K, k0, k1, h);
+        float2 c[4][7];
+        rx_load<CHAN, 4 * g>(c[0], src);
+        rx_load<CHAN, 16 + 4 * g>(c[1], src);
+        rx_load<CHAN, 32 + 4 * g>(c[2], src);
+        rx_load<CHAN, 48 + 4 * g>(c[3], src);
+#ifdef OFDM_RX_EARLY_LOADS
+        sched_fence();
+#endif
+        rx_noisy<NOISE, CHAN, 4 * g>(x, c[0], hd, tb, K, k0, k1, h);
+        rx_noisy<NOISE, CHAN, 16 + 4 * g>(x, c[1], hd, tb, K, k0, k1, h);
+        rx_noisy<NOISE, CHAN, 32 + 4 * g>(x, c[2], hd, tb, K, k0, k1, h);
+        rx_noisy<NOISE, CHAN, 48 + 4 * g>(x, c[3], hd, tb, K, k0, k1, h);
         static_for<0, 4>([&](auto ic) { dif_stage1<false, 4 * g + decltype(ic)::value>(x); });
         sched_fence();
     });
@@ -253,15 +301,17 @@ __device__ __forceinline__ void rx_window_stage1(float2 (&x)[64], const WS &src,
 template <bool DUMP, int KIND, typename HF, typename PF>
 __device__ __forceinline__ void finish_symbol(float2 (&x)[64], const uint32_t (&w)[3], HF &&Hof, PF &&partner,
                                               float2 *dump_eq, uint32_t *dump_bits, bool leader,
-                                              unsigned long long *slots) {
+                                              unsigned long long *slots, RxStamp &sp) {
     SymState st;
     sym_init(st);
     static_for<0, 4>([&](auto rc) {
         constexpr int R = decltype(rc)::value;
         dif_sub16<false, R>(x);
+        sp.mark(1);
         Hof.template prefetch<R>(x);
         demap_sub<DUMP, R, KIND>(x, w, Hof, dump_eq, st);
         sched_fence();
+        sp.mark(2);
     });
     if constexpr (DUMP) {
         if (dump_bits) { dump_bits[0] = st.d[0]; dump_bits[1] = st.d[1]; dump_bits[2] = st.d[2]; }
@@ -270,8 +320,9 @@ __device__ __forceinline__ void finish_symbol(float2 (&x)[64], const uint32_t (&
     const float e_other = __uint_as_float(partner(__float_as_uint(evm)));
     const uint32_t be_other = partner(st.be), ax_other = partner(st.ax);
     FrameAcc acc;
-    if (leader) frame_metrics(acc, evm + e_other, st.be + be_other, st.ax + ax_other);
-    flush_wave(acc, slots);
+    frame_metrics(acc, evm + e_other, st.be + be_other, st.ax + ax_other);   // used on leader lanes only
+    flush_lanes(acc, leader, slots);
+    sp.mark(3);
 }
 
 // ---- LS estimate: a wave carries 21 frames, lanes {E, D0, D1} per frame (lane 63 idle) ----
@@ -302,6 +353,9 @@ struct LsBpermuteEq {
                     __int_as_float(__builtin_amdgcn_ds_bpermute((int)e_addr, __float_as_int(Y.y))));
             }
         });
+#ifdef OFDM_RX_BATCH_BPERM
+        sched_fence();   // issue the sub-block's 24 crossbar reads as one batch, ahead of their uses
+#endif
     }
     template <typename B>
     __device__ __forceinline__ EqOut<2> operator()(float2 Y, B) const {
@@ -337,6 +391,8 @@ __global__ __launch_bounds__(256, OFDM_RX_LS_WAVES) void rx_ls_kernel(RxArgs a) 
     if (grp < n_groups) stage_group<G>(a, grp * LS_GROUP_SYMS, sbuf[0], a.ltf2_rows, wv, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    RxStamp sp;
+    sp.start();
     for (; grp < n_groups; grp += gridDim.x) {
         const int64_t fl = grp * LS_GROUP_FRAMES + fr;
         const bool valid = fr < LS_GROUP_FRAMES && fl < a.n_frames;
@@ -368,6 +424,7 @@ __global__ __launch_bounds__(256, OFDM_RX_LS_WAVES) void rx_ls_kernel(RxArgs a) 
             const float sg = is_e ? a.sigma[q] * 1.41421356237309504880f : a.sigma[q];
             float2 x[64];
             rx_window_stage1<NOISE, CHAN>(x, s, flo, fhi, t0, (uint32_t)(a.q_base + q), sg, a.k0, a.k1, hq);
+            sp.mark(0);
             float2 *dump_eq = nullptr;
             uint32_t *dump_bits = nullptr;
             if constexpr (DUMP) {
@@ -380,12 +437,14 @@ __global__ __launch_bounds__(256, OFDM_RX_LS_WAVES) void rx_ls_kernel(RxArgs a) 
             LsBpermuteEq Hof;
             Hof.e_addr = e_addr;
             auto partner = [&](uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_bpermute((int)d1_addr, (int)v); };
-            finish_symbol<DUMP, 2>(x, wq, Hof, partner, dump_eq, dump_bits, role == 1 && valid, sacc[q]);
+            finish_symbol<DUMP, 2>(x, wq, Hof, partner, dump_eq, dump_bits, role == 1 && valid, sacc[q], sp);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // next group landed
         __syncthreads();                                   // and every wave is done with this one
+        sp.mark(4);
         cur ^= 1;
     }
+    sp.flush(a.stamps);
     block_flush(a, sacc);
 }
 
@@ -404,6 +463,8 @@ __global__ __launch_bounds__(256, OFDM_RX_IDEAL_WAVES) void rx_ideal_kernel(RxAr
     const uint32_t t0 = 336u + 80u * (uint32_t)d;
     const int64_t n_groups = (2 * a.n_frames + 63) / 64;
     const int64_t P = a.pitch;
+    RxStamp sp;
+    sp.start();
     for (int64_t grp = blockIdx.x; grp < n_groups; grp += gridDim.x) {
         stage_group<G>(a, grp * 64, sbuf, nullptr, wv, lane);
         const uint32_t so = (uint32_t)(grp * 64 + lane);
@@ -429,6 +490,7 @@ __global__ __launch_bounds__(256, OFDM_RX_IDEAL_WAVES) void rx_ideal_kernel(RxAr
             }
             float2 x[64];
             rx_window_stage1<NOISE, CHAN>(x, s, flo, fhi, t0, (uint32_t)(a.q_base + q), a.sigma[q], a.k0, a.k1, hq);
+            sp.mark(0);
             float2 *dump_eq = nullptr;
             uint32_t *dump_bits = nullptr;
             if constexpr (DUMP) {
@@ -457,10 +519,12 @@ __global__ __launch_bounds__(256, OFDM_RX_IDEAL_WAVES) void rx_ideal_kernel(RxAr
             };
             auto partner = [](uint32_t v) { return dpp_u<DPP_QUAD_XOR1>(v); };
             auto eq = eq_fn(Hof);
-            finish_symbol<DUMP, KIND>(x, wq, eq, partner, dump_eq, dump_bits, d == 0 && valid, sacc[q]);
+            finish_symbol<DUMP, KIND>(x, wq, eq, partner, dump_eq, dump_bits, d == 0 && valid, sacc[q], sp);
         }
         __syncthreads();                                   // every wave is done with the group
+        sp.mark(4);
     }
+    sp.flush(a.stamps);
     block_flush(a, sacc);
 }
 
@@ -529,6 +593,12 @@ int rx_grid(const ofdm_cfg &cfg, int64_t n_frames, int device) {
         : reinterpret_cast<const void *>(&rx_ideal_kernel<OFDM_CONV_C, OFDM_NOISE_REAL, OFDM_CHAN_AWGN, false>);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1) cus = 256;
+#ifdef OFDM_RX_GRID_ENV   // diagnostic builds: OFDM_RX_BLOCKS_PER_CU caps the resident blocks per CU
+    if (const char *e = getenv("OFDM_RX_BLOCKS_PER_CU")) {
+        const int v = atoi(e);
+        if (v >= 1 && v < per_cu) per_cu = v;
+    }
+#endif
     const int64_t cap = (int64_t)per_cu * cus;
     const int64_t g = need < cap ? need : cap;
     return (int)(g < 1 ? 1 : g);

@@ -173,12 +173,15 @@ def main():
     ap.add_argument("--mc-trials", type=int, default=8000)
     ap.add_argument("--procs", type=int, default=8)
     ap.add_argument("--skip-mc", action="store_true")
-    ap.add_argument("--only", choices=["genie"], help="regenerate one fixture only")
+    ap.add_argument("--only", choices=["genie", "mc"], help="regenerate one fixture only")
     a = ap.parse_args()
     build_ref()
     R = RefLib()
     if a.only == "genie":
         gen_genie(R)
+        return
+    if a.only == "mc":
+        gen_mc(a.mc_trials, a.procs)
         return
     gen_fft(R); gen_tx(R); gen_rx(R); gen_kat(); gen_genie(R)
     if not a.skip_mc:
