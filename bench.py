@@ -228,7 +228,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": pmc.get("rx_hbm_bytes_per_launch"),
-                         "kernel": "frame_rx_kernel" if frame_mode
+                         "kernel": "frame_sync_kernel+frame_sym_kernel" if frame_mode
                                    else ("rx_ls_kernel" if kw.get("est") == "ls" else "rx_ideal_kernel"),
                          "bytes_per_unit": bytes_per_unit,
                          "units_per_launch": units_per_launch,

@@ -18,7 +18,7 @@ from collections import defaultdict
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-KERNELS = ("rx_ls_kernel", "rx_ideal_kernel", "tx_symbols_kernel", "frame_rx_kernel")
+KERNELS = ("rx_ls_kernel", "rx_ideal_kernel", "tx_symbols_kernel", "frame_sync_kernel", "frame_sym_kernel")
 BYTES_PER_UNIT = 652
 CUS, SIMDS, XCDS = 256, 4, 8
 NOMINAL_CLOCK = 2.4e9
@@ -63,7 +63,7 @@ def main(argv):
     trace = read_trace(d)
     summary = json.loads(out.read_text()) if out.exists() else {}
     # the receiver kernel of this run (symbol-mode LS / ideal, or frame mode)
-    rx = next(k for k in ("rx_ls_kernel", "rx_ideal_kernel", "frame_rx_kernel") if k in vals)
+    rx = next(k for k in ("rx_ls_kernel", "rx_ideal_kernel", "frame_sync_kernel") if k in vals)
     c = {k: statistics.mean(v) for k, v in vals[rx].items()}
     t = trace.get(rx, {}).get("avg_ns", float("nan")) * 1e-9
     rd = 2.0 * c.get("FETCH_SIZE", float("nan")) * 1024

@@ -52,6 +52,46 @@
 #define PKF(A, B) "v_pk_fma_f32 v[" #A ":" #B "], v[2:3], v[4:5], v[6:7]\n"
 #define PKA(A, B) "v_pk_add_f32 v[" #A ":" #B "], v[2:3], v[4:5]\n"
 
+#define D0(D) "v_add_f32 v" #D ", s20, v1\n"             // VOP2, SGPR
+#define D1(D) "v_add_f32 v" #D ", 1.0, v1\n"             // VOP2, inline constant
+#define D2(D) "v_mul_f32 v" #D ", 0x3f3504f3, v1\n"      // VOP2, literal
+#define D3(D) "v_lshlrev_b32 v" #D ", 6, v1\n"           // VOP2, inline integer
+#define D4(D) "v_xor_b32 v" #D ", s20, v1\n"             // VOP2, SGPR
+#define D5(D) "v_alignbit_b32 v" #D ", v1, v2, v3\n"     // VOP3, all VGPR
+#define D6(D) "v_fma_f32 v" #D ", -v1, v2, v3\n"         // VOP3, neg modifier
+#define D7(D) "v_mul_f32_e64 v" #D ", v1, -v2\n"         // VOP3 form of a VOP2 op
+#define D8(D) "v_cvt_f32_u32 v" #D ", v1\n"              // VOP1
+#define D9(D) "v_mov_b32_dpp v" #D ", v1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+#define D10(D) "v_cndmask_b32_e64 v" #D ", v1, v2, s[22:23]\n"
+#define D11(D) "v_log_f32 v" #D ", v1\n"
+#define D12(D) "v_add_u32 v" #D ", v1, v2\n"
+#define D13(D) "v_fmac_f32 v" #D ", s20, v1\n"           // VOP2 fmac, SGPR
+#define D14(D) "v_fma_f32 v" #D ", v1, v2, 1.0\n"        // VOP3, inline constant
+#define D15(D) "v_mov_b32 v" #D ", s20\n"                // VOP1, SGPR
+#define D16(D) "v_add_f32 v" #D ", v1, v2\n v_fma_f32 v" #D ", v1, s20, v2\n"   // mixed pair
+#define D17(D) "v_rcp_f32 v" #D ", v1\n"
+#define D18(D) "v_bitop3_b32 v" #D ", v1, v2, v9 bitop3:0x78\n"
+#define MV(A, B) "v_mad_u64_u32 v[" #A ":" #B "], s[22:23], v1, v2, v[4:5]\n"    // all VGPR
+#define MZ(A, B) "v_mad_u64_u32 v[" #A ":" #B "], s[22:23], v1, v2, 0\n"         // VGPR x VGPR + 0
+
+#define F0(D) "v_or_b32 v" #D ", 0x3f800000, v1\n"       // VOP2 int, literal
+#define F1(D) "v_and_b32 v" #D ", v1, v2\n"              // VOP2 int, VGPR
+#define F2(D) "v_xor_b32 v" #D ", v1, v2\n"
+#define F3(D) "v_lshlrev_b32 v" #D ", v1, v2\n"          // shift, VGPR amount
+#define F4(D) "v_mul_lo_u32 v" #D ", v1, v2\n"
+#define F5(D) "v_mul_hi_u32 v" #D ", v1, v2\n"
+#define F6(D) "v_max_f32 v" #D ", v1, v2\n"
+#define F7(D) "v_cvt_i32_f32 v" #D ", v1\n"
+#define F8(D) "v_sub_u32 v" #D ", v1, v2\n"
+#define F9(D) "v_bfe_u32 v" #D ", v1, v2, v3\n"
+#define F10(D) "v_add3_u32 v" #D ", v1, v2, v3\n"
+#define F11(D) "v_mul_u32_u24 v" #D ", v1, v2\n"
+#define F12(D) "v_lshl_or_b32 v" #D ", v1, v2, v3\n"
+#define F13(D) "v_perm_b32 v" #D ", v1, v2, v3\n"
+#define F14(D) "v_rndne_f32 v" #D ", v1\n"
+#define F15(D) "v_sqrt_f32 v" #D ", v1\n"
+#define SH64(A, B) "v_lshlrev_b64 v[" #A ":" #B "], v1, v[2:3]\n"
+
 #define KERNEL(NAME, BODY)                                                                            \
     __global__ __launch_bounds__(256) void NAME(unsigned long long *cyc) {                           \
         __syncthreads();                                                                              \
@@ -81,13 +121,64 @@ KERNEL(k16, P64(M64))
 KERNEL(k17, P64(PKF))
 KERNEL(k18, P64(PKA))
 
+KERNEL(e0, R64(D0))
+KERNEL(e1, R64(D1))
+KERNEL(e2, R64(D2))
+KERNEL(e3, R64(D3))
+KERNEL(e4, R64(D4))
+KERNEL(e5, R64(D5))
+KERNEL(e6, R64(D6))
+KERNEL(e7, R64(D7))
+KERNEL(e8, R64(D8))
+KERNEL(e9, R64(D9))
+KERNEL(e10, R64(D10))
+KERNEL(e11, R64(D11))
+KERNEL(e12, R64(D12))
+KERNEL(e13, R64(D13))
+KERNEL(e14, R64(D14))
+KERNEL(e15, R64(D15))
+KERNEL(e16, R64(D16))
+KERNEL(e17, R64(D17))
+KERNEL(e18, R64(D18))
+KERNEL(e19, P64(MV))
+KERNEL(e20, P64(MZ))
+
+KERNEL(f0, R64(F0))
+KERNEL(f1, R64(F1))
+KERNEL(f2, R64(F2))
+KERNEL(f3, R64(F3))
+KERNEL(f4, R64(F4))
+KERNEL(f5, R64(F5))
+KERNEL(f6, R64(F6))
+KERNEL(f7, R64(F7))
+KERNEL(f8, R64(F8))
+KERNEL(f9, R64(F9))
+KERNEL(f10, R64(F10))
+KERNEL(f11, R64(F11))
+KERNEL(f12, R64(F12))
+KERNEL(f13, R64(F13))
+KERNEL(f14, R64(F14))
+KERNEL(f15, R64(F15))
+KERNEL(f16, P64(SH64))
+
 typedef void (*kfn)(unsigned long long *);
-static const kfn K[] = {k0, k1, k2, k3, k4, k5, k6, k7, k8, k9, k10, k11, k12, k13, k14, k15, k16, k17, k18};
+static const kfn K[] = {k0, k1, k2, k3, k4, k5, k6, k7, k8, k9, k10, k11, k12, k13, k14, k15, k16, k17, k18,
+                        e0, e1, e2, e3, e4, e5, e6, e7, e8, e9, e10, e11, e12, e13, e14, e15, e16, e17, e18, e19, e20,
+                        f0, f1, f2, f3, f4, f5, f6, f7, f8, f9, f10, f11, f12, f13, f14, f15, f16};
 static const char *N[] = {"fma v1,v2,v3 (banks 1,2,3)", "fma v4,v8,v12 (all bank 0)", "fma v4,v8,v1 (two bank 0)",
                           "fma v1,v1,v2 (src0==src1)", "fma v1,v2,v2 (src1==src2)", "fma v1,s20,v2 (SGPR)",
                           "add v1,v2", "add v4,v8 (same bank)", "bitop3 v1,v2,v3", "bitop3 v1,v2,s20",
                           "fmac v,v1,v2 (dst = src2)", "mul v1,v2", "fmamk v1,K,v2", "cndmask v1,v2,vcc",
-                          "sin v1", "alignbit v1,v2,31", "mad_u64_u32 v1,s20", "pk_fma 3 pairs", "pk_add 2 pairs"};
+                          "sin v1", "alignbit v1,v2,31", "mad_u64_u32 v1,s20", "pk_fma 3 pairs", "pk_add 2 pairs",
+                          "add s20,v1 (VOP2 SGPR)", "add 1.0,v1 (VOP2 inline)", "mul lit,v1 (VOP2 literal)",
+                          "lshlrev 6,v1 (VOP2 inline)", "xor s20,v1 (VOP2 SGPR)", "alignbit v1,v2,v3 (VGPR)",
+                          "fma -v1,v2,v3 (modifier)", "mul_e64 v1,-v2", "cvt_f32_u32 v1", "mov_dpp quad_perm",
+                          "cndmask_e64 v1,v2,s[22:23]", "log v1", "add_u32 v1,v2", "fmac s20,v1 (VOP2 SGPR)",
+                          "fma v1,v2,1.0 (VOP3 inline)", "mov s20 (VOP1 SGPR)", "pair: add + fma(SGPR)",
+                          "rcp v1", "bitop3 v1,v2,v9 (VGPR mask)", "mad_u64 v1,v2,v[4:5]", "mad_u64 v1,v2,0",
+                          "or lit,v1", "and v1,v2", "xor v1,v2", "lshlrev v1,v2", "mul_lo_u32", "mul_hi_u32",
+                          "max_f32", "cvt_i32_f32", "sub_u32", "bfe_u32", "add3_u32", "mul_u32_u24",
+                          "lshl_or_b32", "perm_b32", "rndne_f32", "sqrt_f32", "lshlrev_b64"};
 
 int main() {
     hipDeviceProp_t p;
