@@ -130,19 +130,21 @@ def _snr_at(snr, ber, level):
 @pytest.mark.slow
 def test_reference_ber_curve_within_tenth_db(engine, pkg):
     """north_star: reproduce the reference BER-vs-SNR curve within +-0.1 dB.  Reference curve =
-    the compiled OFDM.c's own trial loop, 8000 trials/point (ref_mc_curve.json); GPU: 200k trials."""
-    rows = json.loads((GOLDEN / "ref_mc_curve.json").read_text())["rows"]
-    snr = np.array([r["snr_db"] for r in rows if r["snr_db"] <= 14])
-    ref = np.array([r["ber"] for r in rows if r["snr_db"] <= 14])
+    the compiled OFDM.c's own trial loop, 48000 trials/point (ref_mc_curve.json); GPU: 200k trials."""
+    rows = [r for r in json.loads((GOLDEN / "ref_mc_curve.json").read_text())["rows"] if r["snr_db"] <= 14]
+    snr = np.array([r["snr_db"] for r in rows])
+    ref = np.array([r["ber"] for r in rows])
+    n_ref = np.array([r["trials"] for r in rows])
     c = engine.frame_sweep(pkg.make_cfg(payload="message"), snr, 200_000)
     ber = c[:, 3] / c[:, 2]
     for level in (-1.0, -1.5, -2.0, -2.5):
         s_ref, s_gpu = _snr_at(snr, ref, level), _snr_at(snr, ber, level)
         assert s_ref is not None and s_gpu is not None
-        assert abs(s_ref - s_gpu) < 0.15, (level, s_ref, s_gpu)
-    # and point-wise within the reference's own sampling error (frame-clustered)
-    for s, b, r in zip(snr, ber, ref):
-        sd = math.sqrt(max(r, 1e-4) * 0.5 / 8000)
+        print(f"BER 1e{level}: reference {s_ref:.3f} dB, GPU {s_gpu:.3f} dB, offset {s_gpu - s_ref:+.3f} dB")
+        assert abs(s_ref - s_gpu) < 0.1, (level, s_ref, s_gpu)
+    # and point-wise within the sampling error (frame-clustered: a failed sync costs ~half the bits)
+    for s, b, r, n in zip(snr, ber, ref, n_ref):
+        sd = math.sqrt(max(r, 1e-4) * 0.5 / n + max(b, 1e-4) * 0.5 / 200_000)
         assert abs(b - r) < 6 * sd + 2e-4, (s, b, r)
 
 
