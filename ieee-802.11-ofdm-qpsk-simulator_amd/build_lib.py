@@ -26,9 +26,14 @@ CFLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-fno-slp-vecto
           "-mllvm", "-amdgpu-atomic-optimizer-strategy=None", f"-I{INCLUDE}", f"-I{CSRC}"]
 
 
+# per-source flags: the symbol-mode kernels schedule for ILP (A/B: c3 +1 %, c2 +3 %, c5 +3 %; the
+# frame kernels -0.5 %, profiles/r01/ab/ab_*_ilp.json)
+SOURCE_FLAGS = {"ofdm_symbol.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]}
+
+
 def _compile(src: str, extra: list[str], build_dir: Path = BUILD) -> Path:
     obj = build_dir / (Path(src).stem + ".o")
-    cmd = [HIPCC, *CFLAGS, *extra, "-c", str(CSRC / src), "-o", str(obj)]
+    cmd = [HIPCC, *CFLAGS, *SOURCE_FLAGS.get(src, []), *extra, "-c", str(CSRC / src), "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-6000:]}")

@@ -306,7 +306,10 @@ __device__ __forceinline__ int block_min_i(int v, int *red) {
     return min(red[0], red[1]);
 }
 
-__global__ __launch_bounds__(SYNC_THREADS) void frame_sync_kernel(FrameArgs a) {
+#ifndef FRAME_SYNC_MINB
+#define FRAME_SYNC_MINB 3   // 3 waves/SIMD: +1.3 % (profiles/r01/ab/ab_frame_sync3.json)
+#endif
+__global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kernel(FrameArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
     const int L = a.cap_len, Lc = L - 47;       // Packet_Detection length (OFDM.c:663)
     const int nfr = fr_len(a.n_data);

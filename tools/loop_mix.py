@@ -11,7 +11,7 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 PKG = ROOT / "ieee-802.11-ofdm-qpsk-simulator_amd"
 sys.path.insert(0, str(PKG))
-from build_lib import CFLAGS, HIPCC  # noqa: E402
+from build_lib import CFLAGS, HIPCC, SOURCE_FLAGS  # noqa: E402
 
 # issue cost (SIMD cycles per wave-instruction, 2 waves/SIMD) measured by tools/ubench_valu.hip
 COST2 = {"transc": 8.34, "mad64": 5.02, "dpp": 4.45, "3src": 4.33, "2src": 2.73}
@@ -36,7 +36,7 @@ def cat(op):
 def main(argv):
     pat = argv[0]
     src = PKG / (argv[1] if len(argv) > 1 else "csrc/ofdm_symbol.hip")
-    s = subprocess.run([HIPCC, *CFLAGS, "--cuda-device-only", "-S", str(src), "-o", "-"], capture_output=True,
+    s = subprocess.run([HIPCC, *CFLAGS, *SOURCE_FLAGS.get(src.name, []), "--cuda-device-only", "-S", str(src), "-o", "-"], capture_output=True,
                        text=True, check=True).stdout
     names = [m.group(1) for m in re.finditer(r"^(_Z\S*):", s, re.M) if pat in m.group(1)]
     for name in names:

@@ -16,8 +16,8 @@ def main(argv):
     if not src.is_absolute():
         src = PKG / src
     sys.path.insert(0, str(PKG))
-    from build_lib import CFLAGS, HIPCC
-    cmd = [HIPCC, *CFLAGS, *argv[1:], "-c", str(src), "-o", "/tmp/_ru.o", "-Rpass-analysis=kernel-resource-usage"]
+    from build_lib import CFLAGS, HIPCC, SOURCE_FLAGS
+    cmd = [HIPCC, *CFLAGS, *SOURCE_FLAGS.get(src.name, []), *argv[1:], "-c", str(src), "-o", "/tmp/_ru.o", "-Rpass-analysis=kernel-resource-usage"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode:
         print(r.stderr[-4000:])
