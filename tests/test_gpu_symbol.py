@@ -153,6 +153,27 @@ def test_counters_chunk_and_shard_invariance(engine, pkg):
     assert np.array_equal(a, engine.symbol_sweep(cfg, snrs, n))      # deterministic
 
 
+def test_full_size_c3_invariants(engine, pkg):
+    """BASELINE configs[2] at its full size (1e7 data symbols per SNR point, 16 points 0..30 dB): the
+    counters are bit-identical across chunkings (one 2^23-frame batch, 2^22-frame chunks, odd chunks)
+    and across a two-shard split; exact totals; BER falls monotonically to 0 and the pre-slicer EVM
+    tracks the SNR (-(SNR + 2.17) dB for the genie chain)."""
+    cfg = pkg.make_cfg()
+    snrs = np.arange(0, 31, 2.0)
+    n = 5_000_000
+    a = engine.symbol_sweep(cfg, snrs, n, chunk_frames=1 << 23)
+    assert np.array_equal(a, engine.symbol_sweep(cfg, snrs, n, chunk_frames=1 << 22))
+    assert np.array_equal(a, engine.symbol_sweep(cfg, snrs, n, chunk_frames=1_234_567))
+    half = engine.symbol_sweep(cfg, snrs, 2_500_001) + engine.symbol_sweep(cfg, snrs, n - 2_500_001,
+                                                                          first_frame=2_500_001)
+    assert np.array_equal(a, half)
+    assert np.all(a[:, 0] == n) and np.all(a[:, 1] == 2 * n) and np.all(a[:, 2] == 192 * n)
+    ber = a[:, 3] / a[:, 2]
+    assert np.all(np.diff(ber) <= 0) and ber[0] > 0.1 and np.all(ber[8:] == 0)
+    r = pkg.SweepResult(snrs, a)
+    assert np.all(np.abs(r.evm_pre_db[6:] + snrs[6:] + 2.17) < 0.1), r.evm_pre_db   # >= 12 dB
+
+
 def test_noiseless_full_size(engine, pkg):
     for est in ("ls", "ideal"):
         cfg = pkg.make_cfg(est=est, noise="none")
