@@ -188,9 +188,24 @@ struct StageGeom {
     static constexpr int ROWS = SYM_SAMPLES - R0;
     static constexpr int DATA = DATA_CHUNKS;
     static constexpr int ROW_CHUNKS = DATA_CHUNKS + EXTRA_CHUNKS;
+    static constexpr int LOADED = ROW_CHUNKS;         // chunks per row filled by LDS-DMA
     static constexpr int ROW_F2 = 2 * ROW_CHUNKS;
     static constexpr int CHUNKS = ROWS * ROW_CHUNKS;
     static constexpr int BUF_F2 = ROWS * ROW_F2;
+};
+
+// LS receiver with the 4-tap channel: rows 12..79 of [42 data symbols | 2T chunk | 21 computed
+// columns (each frame's 2T (x) h, fade_group) + 1 pad] float2.  One buffer (35.9 KB): 3 blocks/CU.
+struct FadeGeom {
+    static constexpr int R0 = 12;
+    static constexpr int ROWS = SYM_SAMPLES - R0;
+    static constexpr int DATA = LS_GROUP_SYMS / 2;
+    static constexpr int LOADED = DATA + 1;
+    static constexpr int ROW_CHUNKS = LOADED + 11;
+    static constexpr int ROW_F2 = 2 * ROW_CHUNKS;
+    static constexpr int CHUNKS = ROWS * ROW_CHUNKS;
+    static constexpr int BUF_F2 = ROWS * ROW_F2;
+    static constexpr int ECOL = 2 * LOADED;            // first computed column
 };
 
 // HBM -> LDS by LDS-DMA (global_load_lds_dwordx4: 1 KB per wave-instruction, chunk c lands at LDS
@@ -202,8 +217,8 @@ __device__ __forceinline__ void stage_group(const RxArgs &a, int64_t col0, float
     const float2 *c0 = a.tx + col0;
     for (int k = wv; k * 64 < G::CHUNKS; k += 4) {
         const int c = k * 64 + lane;
-        if (c < G::CHUNKS) {
-            const int row = c / G::ROW_CHUNKS, j = c - row * G::ROW_CHUNKS;
+        const int row = c / G::ROW_CHUNKS, j = c - row * G::ROW_CHUNKS;
+        if (c < G::CHUNKS && j < G::LOADED) {
             const char *src = j < G::DATA ? (const char *)(c0 + (int64_t)(G::R0 + row) * a.pitch) + j * 16
                                           : (const char *)(extra + 2 * (row + G::R0 - 12));
             __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)src,
@@ -325,6 +340,30 @@ __device__ __forceinline__ void finish_symbol(float2 (&x)[64], const uint32_t (&
     sp.mark(3);
 }
 
+// The 4-tap channel y[n] = sum_l h_l x[n - l] (taps < CP) applied once per staged group instead of
+// once per SNR point: it does not depend on the SNR, so the per-SNR loop only adds noise (same fp32
+// operations as rx_noisy's per-SNR form).  Wave v computes the outputs n = 16 v .. 16 v + 15 of column
+// in_col into column out_col; all inputs are read before any output is written.
+template <typename G>
+__device__ __forceinline__ void fade_group(float2 *buf, int wv, int in_col, int out_col, bool active,
+                                           const float2 (&h)[4]) {
+    static_assert(G::R0 == 12, "the channel reaches 3 samples into the cyclic prefix");
+    float2 xv[19];       // x[16 v - 3 + k]: window sample n sits in staged row n + 16 - R0
+    static_for<0, 19>([&](auto kc) {
+        xv[decltype(kc)::value] = buf[(16 * wv + decltype(kc)::value + 1) * G::ROW_F2 + in_col];
+    });
+    __syncthreads();
+    if (active) {
+        static_for<0, 16>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            const float2 y = cadd(cadd(cmul(h[0], xv[i + 3]), cmul(h[1], xv[i + 2])),
+                                  cadd(cmul(h[2], xv[i + 1]), cmul(h[3], xv[i])));
+            buf[(16 * wv + i + 4) * G::ROW_F2 + out_col] = y;
+        });
+    }
+    __syncthreads();
+}
+
 // ---- LS estimate: a wave carries 21 frames, lanes {E, D0, D1} per frame (lane 63 idle) ----
 // H = 0.5 (F1 + F2) conj(Lf) (OFDM.c:830-850) with F1 + F2 = FFT(r1 + r2) (linearity).  Both LTF
 // windows hold the same clean samples T, so the E lane transforms 2T (+ channel) plus the pair's
@@ -370,15 +409,20 @@ struct LsBpermuteEq {
 
 template <int NOISE, int CHAN, bool DUMP>
 __global__ __launch_bounds__(256, OFDM_RX_LS_WAVES) void rx_ls_kernel(RxArgs a) {
-    using G = LsGeom<CHAN>;
+    // 4-tap channel: applied once per group (fade_group) into one buffer, then the SNR loop runs the
+    // AWGN form; no prefetch of the next group (the LDS holds one fading group per block)
+    constexpr bool FADE = CHAN == OFDM_CHAN_RAYLEIGH4;
+    constexpr int LCHAN = FADE ? OFDM_CHAN_AWGN : CHAN;
+    using G = std::conditional_t<FADE, FadeGeom, LsGeom<CHAN>>;
+    constexpr int NBUF = FADE ? 1 : 2;
     __shared__ unsigned long long sacc[OFDM_MAX_SNR][8];
-    __shared__ __attribute__((aligned(16))) float2 sbuf[2][G::BUF_F2];
+    __shared__ __attribute__((aligned(16))) float2 sbuf[NBUF][G::BUF_F2];
     for (int i = threadIdx.x; i < a.n_snr * 8; i += blockDim.x) (&sacc[0][0])[i] = 0ull;
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
     const int fr = lane / 3, role = lane - 3 * fr;     // lane 63: fr 21 (no frame), role 0
     const bool is_e = role == 0;
-    const int col = is_e ? LS_GROUP_SYMS : 2 * fr + role - 1;
+    const int col = is_e ? (FADE ? FadeGeom::ECOL + fr : LS_GROUP_SYMS) : 2 * fr + role - 1;
     // window start on the frame timeline: LTF pair at the LTF1 slots 192, D0 336, D1 416
     const uint32_t t0 = is_e ? 192u : 256u + 80u * (uint32_t)role;
     const uint32_t e_addr = (uint32_t)(3 * fr) << 2;
@@ -406,11 +450,20 @@ __global__ __launch_bounds__(256, OFDM_RX_LS_WAVES) void rx_ls_kernel(RxArgs a) 
         // land the truth words before the prefetch is queued (vmcnt retires in issue order)
         opaque(w[0]); opaque(w[1]); opaque(w[2]);
         float2 h[4] = {make_float2(1.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f)};
-        if constexpr (CHAN == OFDM_CHAN_RAYLEIGH4) channel_taps(f_lo, f_hi, a.k0, a.k1, h);
         const int64_t nxt = grp + gridDim.x;
-        if (nxt < n_groups) stage_group<G>(a, nxt * LS_GROUP_SYMS, sbuf[cur ^ 1], a.ltf2_rows, wv, lane);
+        if constexpr (FADE) {
+            // lane = staged column: 0..41 the data symbols (in place), 42..62 frame lane - 42's 2T (x) h
+            const bool dcol = lane < LS_GROUP_SYMS;
+            const int ff = dcol ? lane >> 1 : lane - LS_GROUP_SYMS;
+            const uint64_t fg = a.first_frame + (uint64_t)(grp * LS_GROUP_FRAMES + ff);
+            float2 hg[4];
+            channel_taps((uint32_t)fg, (uint32_t)(fg >> 32), a.k0, a.k1, hg);
+            fade_group<G>(sbuf[0], wv, dcol ? lane : LS_GROUP_SYMS, dcol ? lane : FadeGeom::ECOL + ff, lane < 63, hg);
+        } else {
+            if (nxt < n_groups) stage_group<G>(a, nxt * LS_GROUP_SYMS, sbuf[cur ^ 1], a.ltf2_rows, wv, lane);
+        }
         LdsRows<G::R0, G::ROW_F2> src;
-        src.base = (lcf2 *)(sbuf[cur] + col);
+        src.base = (lcf2 *)(sbuf[FADE ? 0 : cur] + col);
 
         for (int q = wv; q < a.n_snr; q += 4) {
             LdsRows<G::R0, G::ROW_F2> s = src;
@@ -418,12 +471,9 @@ __global__ __launch_bounds__(256, OFDM_RX_LS_WAVES) void rx_ls_kernel(RxArgs a) 
             uint32_t flo = f_lo, fhi = f_hi;
             float2 hq[4] = {h[0], h[1], h[2], h[3]};
             s.fresh(); opaque(wq[0]); opaque(wq[1]); opaque(wq[2]); opaque(flo); opaque(fhi);
-            if constexpr (CHAN == OFDM_CHAN_RAYLEIGH4) {
-                static_for<0, 4>([&](auto lc) { opaque(hq[decltype(lc)::value].x); opaque(hq[decltype(lc)::value].y); });
-            }
             const float sg = is_e ? a.sigma[q] * 1.41421356237309504880f : a.sigma[q];
             float2 x[64];
-            rx_window_stage1<NOISE, CHAN>(x, s, flo, fhi, t0, (uint32_t)(a.q_base + q), sg, a.k0, a.k1, hq);
+            rx_window_stage1<NOISE, LCHAN>(x, s, flo, fhi, t0, (uint32_t)(a.q_base + q), sg, a.k0, a.k1, hq);
             sp.mark(0);
             float2 *dump_eq = nullptr;
             uint32_t *dump_bits = nullptr;
@@ -439,6 +489,10 @@ __global__ __launch_bounds__(256, OFDM_RX_LS_WAVES) void rx_ls_kernel(RxArgs a) 
             auto partner = [&](uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_bpermute((int)d1_addr, (int)v); };
             finish_symbol<DUMP, 2>(x, wq, Hof, partner, dump_eq, dump_bits, role == 1 && valid, sacc[q], sp);
         }
+        if constexpr (FADE) {
+            __syncthreads();                               // every wave is done with the buffer
+            if (nxt < n_groups) stage_group<G>(a, nxt * LS_GROUP_SYMS, sbuf[0], a.ltf2_rows, wv, lane);
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // next group landed
         __syncthreads();                                   // and every wave is done with this one
         sp.mark(4);
@@ -453,6 +507,8 @@ __global__ __launch_bounds__(256, OFDM_RX_LS_WAVES) void rx_ls_kernel(RxArgs a) 
 // each other's staging) and its 4 waves split the SNR points over them.
 template <int CONV, int NOISE, int CHAN, bool DUMP>
 __global__ __launch_bounds__(256, OFDM_RX_IDEAL_WAVES) void rx_ideal_kernel(RxArgs a) {
+    constexpr bool FADE = CHAN == OFDM_CHAN_RAYLEIGH4;     // channel applied once per group (fade_group)
+    constexpr int LCHAN = FADE ? OFDM_CHAN_AWGN : CHAN;
     using G = StageGeom<CHAN, 32, 0>;
     __shared__ unsigned long long sacc[OFDM_MAX_SNR][8];
     __shared__ __attribute__((aligned(16))) float2 sbuf[G::BUF_F2];
@@ -477,6 +533,7 @@ __global__ __launch_bounds__(256, OFDM_RX_IDEAL_WAVES) void rx_ideal_kernel(RxAr
         if constexpr (CHAN == OFDM_CHAN_RAYLEIGH4) channel_taps(f_lo, f_hi, a.k0, a.k1, h);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();                                   // the group has landed for every wave
+        if constexpr (FADE) fade_group<G>(sbuf, wv, lane, lane, true, h);   // column = lane, its frame's taps
         LdsRows<G::R0, G::ROW_F2> src;
         src.base = (lcf2 *)(sbuf + lane);
         for (int q = wv; q < a.n_snr; q += 4) {
@@ -489,7 +546,7 @@ __global__ __launch_bounds__(256, OFDM_RX_IDEAL_WAVES) void rx_ideal_kernel(RxAr
                 static_for<0, 4>([&](auto lc) { opaque(hq[decltype(lc)::value].x); opaque(hq[decltype(lc)::value].y); });
             }
             float2 x[64];
-            rx_window_stage1<NOISE, CHAN>(x, s, flo, fhi, t0, (uint32_t)(a.q_base + q), a.sigma[q], a.k0, a.k1, hq);
+            rx_window_stage1<NOISE, LCHAN>(x, s, flo, fhi, t0, (uint32_t)(a.q_base + q), a.sigma[q], a.k0, a.k1, hq);
             sp.mark(0);
             float2 *dump_eq = nullptr;
             uint32_t *dump_bits = nullptr;
