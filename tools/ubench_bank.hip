@@ -92,6 +92,11 @@
 #define F15(D) "v_sqrt_f32 v" #D ", v1\n"
 #define SH64(A, B) "v_lshlrev_b64 v[" #A ":" #B "], v1, v[2:3]\n"
 
+#define G0(D) "v_cmp_gt_f32 vcc, v1, v2\n v_cndmask_b32 v" #D ", v1, v2, vcc\n"              // cmp -> cndmask (VCC)
+#define G1(D) "v_cmp_gt_f32_e64 s[22:23], v1, v2\n v_cndmask_b32_e64 v" #D ", v1, v2, s[22:23]\n"   // via SGPR pair
+#define G2(D) "v_cmp_gt_f32 vcc, v1, v2\n"                                             // cmp alone
+#define G3(D) "v_max_f32 v" #D ", v1, v2\n v_min_f32 v" #D ", v" #D ", v3\n"          // max/min pair
+
 #define KERNEL(NAME, BODY)                                                                            \
     __global__ __launch_bounds__(256) void NAME(unsigned long long *cyc) {                           \
         __syncthreads();                                                                              \
@@ -161,10 +166,16 @@ KERNEL(f14, R64(F14))
 KERNEL(f15, R64(F15))
 KERNEL(f16, P64(SH64))
 
+KERNEL(g0, R64(G0))
+KERNEL(g1, R64(G1))
+KERNEL(g2, R64(G2))
+KERNEL(g3, R64(G3))
+
 typedef void (*kfn)(unsigned long long *);
 static const kfn K[] = {k0, k1, k2, k3, k4, k5, k6, k7, k8, k9, k10, k11, k12, k13, k14, k15, k16, k17, k18,
                         e0, e1, e2, e3, e4, e5, e6, e7, e8, e9, e10, e11, e12, e13, e14, e15, e16, e17, e18, e19, e20,
-                        f0, f1, f2, f3, f4, f5, f6, f7, f8, f9, f10, f11, f12, f13, f14, f15, f16};
+                        f0, f1, f2, f3, f4, f5, f6, f7, f8, f9, f10, f11, f12, f13, f14, f15, f16,
+                        g0, g1, g2, g3};
 static const char *N[] = {"fma v1,v2,v3 (banks 1,2,3)", "fma v4,v8,v12 (all bank 0)", "fma v4,v8,v1 (two bank 0)",
                           "fma v1,v1,v2 (src0==src1)", "fma v1,v2,v2 (src1==src2)", "fma v1,s20,v2 (SGPR)",
                           "add v1,v2", "add v4,v8 (same bank)", "bitop3 v1,v2,v3", "bitop3 v1,v2,s20",
@@ -178,7 +189,9 @@ static const char *N[] = {"fma v1,v2,v3 (banks 1,2,3)", "fma v4,v8,v12 (all bank
                           "rcp v1", "bitop3 v1,v2,v9 (VGPR mask)", "mad_u64 v1,v2,v[4:5]", "mad_u64 v1,v2,0",
                           "or lit,v1", "and v1,v2", "xor v1,v2", "lshlrev v1,v2", "mul_lo_u32", "mul_hi_u32",
                           "max_f32", "cvt_i32_f32", "sub_u32", "bfe_u32", "add3_u32", "mul_u32_u24",
-                          "lshl_or_b32", "perm_b32", "rndne_f32", "sqrt_f32", "lshlrev_b64"};
+                          "lshl_or_b32", "perm_b32", "rndne_f32", "sqrt_f32", "lshlrev_b64",
+                          "pair: cmp vcc + cndmask vcc", "pair: cmp_e64 s + cndmask_e64 s", "cmp vcc alone",
+                          "pair: max + min"};
 
 int main() {
     hipDeviceProp_t p;
