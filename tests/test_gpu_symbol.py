@@ -174,6 +174,26 @@ def test_full_size_c3_invariants(engine, pkg):
     assert np.all(np.abs(r.evm_pre_db[6:] + snrs[6:] + 2.17) < 0.1), r.evm_pre_db   # >= 12 dB
 
 
+def test_symbol_edges(engine, oracle, pkg):
+    """Empty sweeps, one frame, LS-group boundaries (21 frames per wave) against the oracle, and the
+    batch-size limit of the Tx/Rx entry points (an error code, never a crash)."""
+    cfg = pkg.make_cfg()
+    assert not engine.symbol_sweep(cfg, [0.0, 10.0], 0).any()                  # no frames
+    assert engine.symbol_sweep(cfg, [], 100).shape == (0, abi_ncounters(pkg))  # no SNR points
+    for nf in (1, 20, 21, 22, 63, 64):
+        g = engine.symbol_sweep(cfg, [0.0, 8.0], nf, first_frame=777)
+        o = oracle.symbol_sweep(oracle.cfg(), [0.0, 8.0], 777, nf)
+        assert np.array_equal(g[:, :3], o[:, :3]), nf
+        assert np.all(np.abs(g[:, 3] - o[:, 3]) <= 2), (nf, g[:, 3], o[:, 3])
+    with pytest.raises(Exception):
+        engine.tx_frames(cfg, 0, (1 << 23) + 1)                               # > MAX_BATCH_FRAMES
+
+
+def abi_ncounters(pkg):
+    from ofdm_amd import abi
+    return abi.NCOUNTERS
+
+
 def test_noiseless_full_size(engine, pkg):
     for est in ("ls", "ideal"):
         cfg = pkg.make_cfg(est=est, noise="none")
