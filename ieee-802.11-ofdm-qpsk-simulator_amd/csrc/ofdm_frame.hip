@@ -291,6 +291,15 @@ __device__ __forceinline__ float block_sum_f(float v, float *red) {
     __syncthreads();
     return red[0] + red[1];
 }
+// the sum of a float pair over the two waves (scratch: 4 slots), in the same order as block_sum_f
+__device__ __forceinline__ float2 block_sum_f2(float2 v, float *red) {
+    v.x = wave_sum_f(v.x);
+    v.y = wave_sum_f(v.y);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) { red[2 * (threadIdx.x >> 6)] = v.x; red[2 * (threadIdx.x >> 6) + 1] = v.y; }
+    __syncthreads();
+    return make_float2(red[0] + red[2], red[1] + red[3]);
+}
 __device__ __forceinline__ int block_max_i(int v, int *red) {
     v = wave_max_i(v);
     __syncthreads();
@@ -526,37 +535,44 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
         FR_STAMP(3);                                           // matched filter + down-sample
 
         // ---- Coarse CFO (OFDM.c:773-804): 16-lag autocorrelation of the short preamble ----
-        float px = 0.f, py = 0.f;
-        if (tid < 16) { const float2 u = fr[80 + tid], v = fr[96 + tid]; px = u.x * v.x + u.y * v.y; py = u.y * v.x - u.x * v.y; }
-        px = block_sum_f(px, redf); py = block_sum_f(py, redf);
-        double fc = (-1.0 / (2.0 * M_PI * 16.0 * TS)) * (double)atan2f(py, px);
-        if (a.float_cfo) fc = (double)(float)fc;
-        for (int k = tid; k < nfr; k += SYNC_THREADS) fr[k] = cfo_rot(fr[k], fc * TS, k);
-        __syncthreads();
-        // ---- Fine CFO (OFDM.c:806-828): 64-lag over the two long training symbols ----
-        px = 0.f; py = 0.f;
-        if (tid < 64) {
-            const float2 u = fr[192 + tid], v = fr[256 + tid];
-            px = u.x * v.x + u.y * v.y;
-            py = u.y * v.x - u.x * v.y;
+        float2 pp = make_float2(0.f, 0.f);
+        if (tid < 16) {
+            const float2 u = fr[80 + tid], v = fr[96 + tid];
+            pp = make_float2(u.x * v.x + u.y * v.y, u.y * v.x - u.x * v.y);
         }
-        px = block_sum_f(px, redf); py = block_sum_f(py, redf);
-        double ff = (-1.0 / (2.0 * M_PI * 64.0 * TS)) * (double)atan2f(py, px);
+        pp = block_sum_f2(pp, redf);
+        double fc = (-1.0 / (2.0 * M_PI * 16.0 * TS)) * (double)atan2f(pp.y, pp.x);
+        if (a.float_cfo) fc = (double)(float)fc;
+        // ---- Fine CFO (OFDM.c:806-828): 64-lag over the two long training symbols after the coarse
+        // rotation; the 128 rotated LTF samples are formed on the fly (the same arithmetic as rotating
+        // the whole frame first) ----
+        pp = make_float2(0.f, 0.f);
+        if (tid < 64) {
+            const float2 u = cfo_rot(fr[192 + tid], fc * TS, 192 + tid), v = cfo_rot(fr[256 + tid], fc * TS, 256 + tid);
+            pp = make_float2(u.x * v.x + u.y * v.y, u.y * v.x - u.x * v.y);
+        }
+        pp = block_sum_f2(pp, redf);
+        double ff = (-1.0 / (2.0 * M_PI * 64.0 * TS)) * (double)atan2f(pp.y, pp.x);
         if (a.float_cfo) ff = (double)(float)ff;
-        for (int k = tid; k < nfr; k += SYNC_THREADS) fr[k] = cfo_rot(fr[k], ff * TS, k);
-        __syncthreads();
-        if (a.dbg_frame && first_item) for (int k = tid; k < nfr; k += SYNC_THREADS) a.dbg_frame[k] = fr[k];
-        FR_STAMP(4);                                           // coarse + fine CFO
-
-        // ---- hand-off: LTF1 [192,256), LTF2 [256,320), data d [336 + 80 d, +64) (OFDM.c:830-850,
-        // 1024-1040), plus the sync outcome ----
+        // ---- both rotations in one pass (coarse, then fine: OFDM.c:802, 825), the result handed off
+        // directly: LTF1 [192,256), LTF2 [256,320), data d [336 + 80 d, +64) (OFDM.c:830-850,
+        // 1024-1040) ----
         const int nw = 2 + a.n_data;
         float2 *dst = a.win + i * (int64_t)(nw * 64);
-        for (int e = tid; e < nw * 64; e += SYNC_THREADS) {
-            const int w = e >> 6, n = e & 63;
-            const int w0 = w == 0 ? 192 : w == 1 ? 256 : 336 + 80 * (w - 2);
-            dst[e] = fr[w0 + n];
+        const bool dbg = a.dbg_frame && first_item;
+        for (int k = tid; k < nfr; k += SYNC_THREADS) {
+            const float2 v = cfo_rot(cfo_rot(fr[k], fc * TS, k), ff * TS, k);
+            if (dbg) a.dbg_frame[k] = v;
+            int w = -1, n = 0;
+            if (k >= 192 && k < 320) {
+                w = (k - 192) >> 6; n = (k - 192) & 63;
+            } else if (k >= 336) {
+                const int d = (k - 336) / 80, o = k - 336 - 80 * d;
+                if (d < a.n_data && o < 64) { w = 2 + d; n = o; }
+            }
+            if (w >= 0) dst[w * 64 + n] = v;
         }
+        FR_STAMP(4);                                           // coarse + fine CFO + hand-off
         if (tid == 0) {
             a.info[i] = make_int4(p, sync_fail, oob, rx_start);
             unsigned long long *sl = acc + q * ACC_SLOTS;
