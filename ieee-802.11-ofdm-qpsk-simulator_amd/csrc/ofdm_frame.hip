@@ -307,6 +307,15 @@ __device__ __forceinline__ int block_max_i(int v, int *red) {
     __syncthreads();
     return max(red[0], red[1]);
 }
+// (min of a, max of b) over the two waves in one exchange (scratch: 4 slots)
+__device__ __forceinline__ int2 block_minmax_i(int a, int b, int *red) {
+    a = wave_min_i(a);
+    b = wave_max_i(b);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) { red[2 * (threadIdx.x >> 6)] = a; red[2 * (threadIdx.x >> 6) + 1] = b; }
+    __syncthreads();
+    return make_int2(min(red[0], red[2]), max(red[1], red[3]));
+}
 __device__ __forceinline__ int block_min_i(int v, int *red) {
     v = wave_min_i(v);
     __syncthreads();
@@ -497,8 +506,9 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
         const int front = (first >= 0 && first - prev > 300) ? first : -1;
         FR_STAMP(1);                                           // packet detection
         const bool valid = front >= 0 && front + 230 < Lc && bit_at(cross, front + 230);
-        const int maxf = block_max_i(front, redi);
-        const int cand = block_min_i((valid && front < maxf) ? front : 0x7fffffff, redi);
+        // the first valid front that has a later front: the least valid front, unless it is the last one
+        const int2 mm = block_minmax_i(valid ? front : 0x7fffffff, front, redi + 4);
+        const int cand = mm.x < mm.y ? mm.x : 0x7fffffff;
         const bool sync_fail = cand == 0x7fffffff;
         const int p = sync_fail ? 0 : cand + 10 + 1;           // len_RRC_rx + 1 (OFDM.c:758)
         FR_STAMP(2);                                           // packet selection
