@@ -439,7 +439,6 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
         // LDS reads issued 8 positions at a time.  M > 0.75 (OFDM.c:687, 695) is tested as
         // num > 0.75 den, which keeps the division's 0/0 -> false and x/0 -> true outcomes. ----
         const int n0 = tid * chunk, n1 = min(n0 + chunk, Lc);
-        int first = -1, last = -1;                  // first / last crossing in this lane's chunk
         unsigned long long cmask = 0ull;            // crossing n at bit n - n0 (chunk <= 64)
         if (n0 < n1) {
             float sx = 0.f, sy = 0.f, pw = 0.f;
@@ -450,30 +449,34 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
                 sy += u.x * v.y + u.y * v.x;
                 pw += v.x * v.x + v.y * v.y;
             }
-            for (int nb = n0; nb < n1; nb += 8) {
-                float2 o0[8], o1[8], i0[8], i1[8];
+            // batches of DET_B positions (the 2961-position capture gives chunks of 25 = 5 x 5); the
+            // batch's crossings are collected with constant shifts and placed once per batch
+            constexpr int DET_B = 5;
+            for (int nb = n0; nb < n1; nb += DET_B) {
+                float2 o0[DET_B], o1[DET_B], i0[DET_B], i1[DET_B];
 #pragma unroll
-                for (int k = 0; k < 8; ++k) {           // reads past the capture land in fr/cross: unused
+                for (int k = 0; k < DET_B; ++k) {       // reads past the capture land in fr/cross: unused
                     o0[k] = r[nb + k]; o1[k] = r[nb + k + 16]; i0[k] = r[nb + k + 32]; i1[k] = r[nb + k + 48];
                 }
+                uint32_t m = 0u;
 #pragma unroll
-                for (int k = 0; k < 8; ++k) {           // branch-free: positions >= n1 are masked off
-                    const int n = nb + k;
+                for (int k = 0; k < DET_B; ++k) {       // branch-free: positions >= n1 are masked off
                     const float num = sx * sx + sy * sy, den = pw * pw;
-                    const bool cr = n < n1 && num > 0.75f * den;
-                    cmask |= cr ? 1ull << (n - n0) : 0ull;
-                    first = (cr && first < 0) ? n : first;
-                    last = cr ? n : last;
+                    m |= (nb + k < n1 && num > 0.75f * den) ? 1u << k : 0u;
                     sx += (i0[k].x * i1[k].x - i0[k].y * i1[k].y) - (o0[k].x * o1[k].x - o0[k].y * o1[k].y);
                     sy += (i0[k].x * i1[k].y + i0[k].y * i1[k].x) - (o0[k].x * o1[k].y + o0[k].y * o1[k].x);
                     pw += (i1[k].x * i1[k].x + i1[k].y * i1[k].y) - (o1[k].x * o1[k].x + o1[k].y * o1[k].y);
                 }
+                cmask |= (unsigned long long)m << (nb - n0);
             }
             if (cmask) {
                 atomicOr(&cross[n0 >> 6], cmask << (n0 & 63));
                 if ((n0 & 63) + chunk > 64) atomicOr(&cross[(n0 >> 6) + 1], cmask >> (64 - (n0 & 63)));
             }
         }
+        // first / last crossing in this lane's chunk
+        const int first = cmask ? n0 + __builtin_ctzll(cmask) : -1;
+        const int last = cmask ? n0 + 63 - __builtin_clzll(cmask) : -1;
         if (a.dbg_corr && first_item) {             // Corr_Out for ofdm_receiver's parity dump
             for (int n = tid; n < Lc; n += SYNC_THREADS) {
                 float sx = 0.f, sy = 0.f, pw = 0.f;
