@@ -266,7 +266,10 @@ __device__ __forceinline__ float2 cfo_rot(float2 v, double f_ts, int i) {
     const double rev = -f_ts * (double)i;
     const float fr = (float)(rev - rint(rev));
     float s, c;
-    sincospif(2.0f * fr, &s, &c);
+    // v_sin/v_cos take revolutions; |fr| <= 0.5 is inside their accurate range, and one
+    // transcendental each replaces sincospif's range reduction and polynomials (+6 % frame mode)
+    s = __builtin_amdgcn_sinf(fr);
+    c = __builtin_amdgcn_cosf(fr);
     return make_float2(v.x * c - v.y * s, v.x * s + v.y * c);
 }
 
