@@ -54,6 +54,7 @@ struct FrameArgs {
     int64_t n_trials;
     int32_t n_snr, q_base;
     int32_t cap_len, float_cfo, matlab, fixed_start, noise, wave_len, n_data, word_stats;
+    int32_t fr_in_cap;              // fr[] inside the capture region (fr_in_capture)
     uint32_t k0, k1;
     uint32_t table[3 * FR_MAX_DATA];
     unsigned long long *counters;   // [n_snr][OFDM_NCOUNTERS]
@@ -281,9 +282,21 @@ __host__ __device__ inline int cross_words(int cap_len) { return (cap_len - 47 +
 // capture region: cap_len + 8 samples, the capture starting at sample (rx_start & 3) so that every
 // Philox block of 4 samples is a 16-byte aligned pair of ds_write_b128
 __host__ __device__ inline int cap_region(int cap_len) { return (cap_len + 8 + 1) & ~1; }
+// The filtered frame fr[] goes into the part of the capture region the matched filter does not read:
+// it reads 2 nfr + 19 samples, so the unread prefix or suffix holds nfr samples whenever the region has
+// 4 nfr + 19 (every default capture).  Shorter user captures get fr[] after the scratch words instead.
+// (-3.8 KB per trial for the reference capture: 6 instead of 5 blocks per CU.)
+__host__ __device__ inline bool fr_in_capture(int cap_len, int n_data) {
+    return cap_region(cap_len) >= 4 * fr_len(n_data) + 20;
+}
 __host__ __device__ inline size_t frame_lds_bytes(int cap_len, int n_data, int n_snr) {
-    return (size_t)cap_region(cap_len) * 8 + (size_t)fr_len(n_data) * 8 + (size_t)cross_words(cap_len) * 8 +
-           (size_t)n_snr * ACC_SLOTS * 8 + 64;
+#ifdef OFDM_FR_SEPARATE
+    const bool in_cap = false;
+#else
+    const bool in_cap = fr_in_capture(cap_len, n_data);
+#endif
+    return (size_t)cap_region(cap_len) * 8 + (size_t)cross_words(cap_len) * 8 + (size_t)n_snr * ACC_SLOTS * 8 + 64 +
+           (in_cap ? 0 : (size_t)fr_len(n_data) * 8);
 }
 
 // block-wide reductions over the two waves (scratch: 2 slots in `red`)
@@ -336,11 +349,12 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
     const int nfr = fr_len(a.n_data);
     const int tid = threadIdx.x, lane = tid & 63;
     float2 *rbase = reinterpret_cast<float2 *>(smem);
-    float2 *fr = rbase + cap_region(L);
-    unsigned long long *cross = reinterpret_cast<unsigned long long *>(fr + nfr);
+    unsigned long long *cross = reinterpret_cast<unsigned long long *>(rbase + cap_region(L));
     unsigned long long *acc = cross + cross_words(L);
     float *redf = reinterpret_cast<float *>(acc + a.n_snr * ACC_SLOTS);
     int *redi = reinterpret_cast<int *>(redf + 4);
+    float2 *const fr_sep = reinterpret_cast<float2 *>(redf + 16);   // used when !fr_in_capture
+    float2 *fr = fr_sep;
     for (int i = tid; i < a.n_snr * ACC_SLOTS; i += SYNC_THREADS) {
         const int k = i % ACC_SLOTS;
         acc[i] = k == 10 ? (unsigned long long)INT64_MAX : k == 11 ? (unsigned long long)INT64_MIN : 0ull;
@@ -522,6 +536,11 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
         const int p = sync_fail ? 0 : cand + 10 + 1;           // len_RRC_rx + 1 (OFDM.c:758)
         FR_STAMP(2);                                           // packet selection
 
+        // fr[] in the unread prefix [0, off + lo) or suffix (off + hi, region) of the capture region
+        if (a.fr_in_cap) {
+            const int off = rx_start & 3, lo = max(p - 20, 0), hi = min(p + 2 * nfr - 2, L - 1);
+            fr = off + lo >= nfr ? rbase : rbase + off + hi + 1;
+        }
         // ---- RRC matched filter at the down-sampled instants p + 2i (OFDM.c:965, 992-996): outputs
         // interleaved over the lanes, so a tap's reads are 2 samples apart across lanes (no bank
         // conflicts); clamped reads + select are Convolution's zero padding ----
@@ -552,7 +571,7 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
                     v.y = fmaf(x.y, tv[j], v.y);
                 }
             }
-            fr[ii] = v;
+            fr[ii] = v;                                          // outside every lane's reads
         }
         const bool oob = block_max_i(oob_l ? 1 : 0, redi) != 0;   // also orders fr[] for every lane
         FR_STAMP(3);                                           // matched filter + down-sample
@@ -841,6 +860,11 @@ static int run_frame_chunk(Ctx *c, FrameArgs &a) {
     a.win = (float2 *)c->d_scratch;
     a.info = (int4 *)((char *)c->d_scratch + ((wbytes + 255) & ~size_t(255)));
     const size_t lds = frame_lds_bytes(a.cap_len, a.n_data, a.n_snr);
+#ifdef OFDM_FR_SEPARATE
+    a.fr_in_cap = 0;
+#else
+    a.fr_in_cap = fr_in_capture(a.cap_len, a.n_data);
+#endif
     hipLaunchKernelGGL(frame_sync_kernel,
                        dim3(occupancy_grid(reinterpret_cast<const void *>(&frame_sync_kernel), SYNC_THREADS, lds,
                                            c->cus, a.n_items)),

@@ -197,12 +197,16 @@ class Engine:
         return dict(min=float(out[0]), max=float(out[1]), max_abs=float(out[2]), bits=bits.value)
 
     def frame_sweep(self, cfg: Cfg, snr_db, n_trials: int, first_trial: int = 0, mode: str = "c",
-                    fixed_start: int = -1, want_packet_idx: bool = False, word_stats: bool = False):
+                    fixed_start: int = -1, want_packet_idx: bool = False, word_stats: bool = False,
+                    cap_len: int = 0):
+        """cap_len 0: the mode's capture (int(0.307 len), OFDM.c:945; 3000 for 'matlab')."""
         snr = np.ascontiguousarray(snr_db, np.float64)
         out = np.zeros((len(snr), abi.NCOUNTERS), np.int64)
         pidx = np.zeros((len(snr), n_trials), np.int32) if want_packet_idx else None
         opts = make_rx_opts(mode, fixed_start)
         opts.word_stats = int(word_stats)
+        if cap_len:
+            opts.cap_len = int(cap_len)
         check(self.lib, self.lib.ofdm_frame_sweep(self.ctx, C.byref(cfg), C.byref(opts), snr.ctypes.data_as(C.c_void_p),
                                                   len(snr), first_trial, n_trials, out.ctypes.data_as(C.c_void_p),
                                                   None if pidx is None else pidx.ctypes.data_as(C.c_void_p)),

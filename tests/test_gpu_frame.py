@@ -118,6 +118,24 @@ def test_frame_sweep_noiseless_and_edges(engine, pkg):
         engine.frame_sweep(pkg.make_cfg(payload="random"), [10.0], 10)   # needs a fixed payload
 
 
+def test_frame_sweep_capture_lengths(engine, pkg):
+    """The filtered frame shares the capture's LDS region when the region has 4 nfr + 20 samples
+    (1970: tight fit, 3008: default) and has its own region otherwise (1500).  With the first frame
+    at capture sample 400 and the next at 1380, every length selects the same packet, and the
+    waveform-indexed noise makes the frame samples identical: all counters agree."""
+    cfg_n = pkg.make_cfg(payload="message", noise="none")
+    cfg = pkg.make_cfg(payload="message")
+    for c, snrs in ((cfg_n, [20.0]), (cfg, [16.0, 20.0])):
+        res = [engine.frame_sweep(c, snrs, 64, fixed_start=580, want_packet_idx=True, cap_len=L)
+               for L in (1500, 1970, 3008)]
+        for cnt, pidx in res[1:]:
+            assert np.array_equal(pidx, res[0][1])
+            assert np.array_equal(cnt, res[0][0])
+        assert np.all(res[0][1] > 0)
+        if c is cfg_n:
+            assert np.all(res[0][1] == res[0][1][0, 0]) and res[0][0][0, 3] == 0
+
+
 def _snr_at(snr, ber, level):
     """SNR where log10(BER) crosses `level` (linear interpolation of log BER)."""
     lb = np.log10(np.maximum(ber, 1e-12))
