@@ -649,7 +649,10 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
 // broadcasts), ceil(n_data / 2) quads per item, 16 quads per wave.
 constexpr int SYM_THREADS = 256;
 template <bool DUMP>   // DUMP: item 0's bits / subcarriers / metrics for ofdm_receiver
-__global__ __launch_bounds__(SYM_THREADS, 2) void frame_sym_kernel(FrameArgs a) {
+#ifndef FRAME_SYM_MINB
+#define FRAME_SYM_MINB 2   // 3 waves/SIMD spills 196 VGPRs: frame mode 9 % slower
+#endif
+__global__ __launch_bounds__(SYM_THREADS, FRAME_SYM_MINB) void frame_sym_kernel(FrameArgs a) {
     __shared__ unsigned long long acc[OFDM_MAX_SNR][8];
     __shared__ float part_e[SYM_THREADS / 4][2];             // per quad: EVM of its two data symbols
     __shared__ uint32_t part_b[SYM_THREADS / 4][2], part_a[SYM_THREADS / 4][2];
