@@ -245,6 +245,14 @@ class SweepResult:
         return c[:, abi.C_EVMDB_PRE_Q] / abi.EVM_Q_SCALE / np.maximum(c[:, abi.C_FRAMES], 1)
 
     @property
+    def mean_frame_evm_post_db(self) -> np.ndarray:
+        """mean over frames of the per-frame post-slicer EVM_dB (OFDM.c:1150); -inf when any frame
+        had no slicer error (that frame's own value is -inf, OFDM.c:1148-1150)"""
+        c = self.counters
+        m = c[:, abi.C_EVMDB_POST_Q] / abi.EVM_Q_SCALE / np.maximum(c[:, abi.C_FRAMES], 1)
+        return np.where(c[:, abi.C_EVMDB_POST_FINITE] < c[:, abi.C_FRAMES], -np.inf, m)
+
+    @property
     def sync_fail_rate(self) -> np.ndarray:
         c = self.counters
         return c[:, abi.C_SYNC_FAIL] / np.maximum(c[:, abi.C_FRAMES], 1)

@@ -8,8 +8,16 @@ runs unchanged.  The reference runs ONE trial per SNR point (frame mode, fixed m
 EVM = 10 log10(sum|e|^2 / sum|d|^2)); with trials=1 they equal the reference's per-trial values.
 `mode="symbol"` runs the per-symbol chain (genie timing, LTF LS estimate) instead.
 
+Per-point values in the files.  Output_EVM_AGC.txt / Output_EVM_AGC_DB.txt hold, for trials > 1,
+the MEAN over trials of the per-trial EVM_dB the reference writes for its one trial
+(OFDM.c:1126,1150); the post-slicer mean is -inf as soon as one trial had no slicer error, as the
+reference's own value for that trial is (ref_mc_curve.json's mean_evm_agc_db is the same
+statistic).  evm="pooled" writes 10 log10(sum|e|^2 / sum|d|^2) over all trials instead.  BER is
+errors / bits (= the mean per-trial BER: every trial carries the same bit count).
+
 Multi-GPU: launched under torchrun, each rank takes a contiguous share of the trials
-(dist.shard_range) and the counters are summed with one all-reduce before rank 0 writes.
+(dist.shard_range); reference_main() forms the process group (dist.init_from_env: RCCL, or gloo
+with OFDM_DIST_BACKEND=gloo) and the counters are summed with one all-reduce before rank 0 writes.
 """
 from __future__ import annotations
 
@@ -44,25 +52,32 @@ def run_sweep(engine: Engine, snr_db, trials: int, mode: str = "frame", seed: in
     else:
         raise ValueError(mode)
     if world > 1:
-        import torch  # noqa: PLC0415
-        t = torch.from_numpy(c).to(f"cuda:{engine.device}")
-        dist.allreduce_counters(t)
-        c = t.cpu().numpy()
+        c = dist.allreduce_counters_np(c, engine.device)
     return SweepResult(snr, c)
 
 
 def reference_main(out_dir: str | Path = "data", trials: int = 1, mode: str = "frame", snr_db=REF_SNR,
-                   seed: int = 0x80211A, device: int = 0, json_sidecar: bool = True, **kw) -> SweepResult:
+                   seed: int = 0x80211A, device: int = 0, json_sidecar: bool = True, evm: str = "trial",
+                   **kw) -> SweepResult:
+    if evm not in ("trial", "pooled"):
+        raise ValueError(evm)
     rank, world, local = dist.env_rank_world()
+    if world > 1:
+        dist.init_from_env()
     t0 = time.perf_counter()
     with Engine(local if world > 1 else device) as eng:
         res = run_sweep(eng, snr_db, trials, mode=mode, seed=seed, rank=rank, world=world, **kw)
     wall = time.perf_counter() - t0
     if rank == 0:
-        write_reference_outputs(out_dir, res.snr_db, res.evm_pre_db, res.evm_post_db, res.ber)
+        pre, post = ((res.mean_frame_evm_db, res.mean_frame_evm_post_db) if evm == "trial"
+                     else (res.evm_pre_db, res.evm_post_db))
+        write_reference_outputs(out_dir, res.snr_db, pre, post, res.ber)
         if json_sidecar:
             side = {"mode": mode, "trials_per_snr": trials, "world": world, "seed": seed, "wall_s": wall,
-                    "snr_db": res.snr_db.tolist(), "ber": res.ber.tolist(), "evm_pre_db": res.evm_pre_db.tolist(),
+                    "evm_files": evm, "snr_db": res.snr_db.tolist(), "ber": res.ber.tolist(),
+                    "mean_trial_evm_db": res.mean_frame_evm_db.tolist(),
+                    "mean_trial_evm_post_db": [float(v) for v in res.mean_frame_evm_post_db],
+                    "evm_pre_db": res.evm_pre_db.tolist(),
                     "evm_post_db": [float(v) for v in res.evm_post_db], "sync_fail_rate": res.sync_fail_rate.tolist(),
                     "counters": res.counters.tolist()}
             (Path(out_dir) / "ofdm_sweep.json").write_text(json.dumps(side, indent=1))
@@ -82,12 +97,14 @@ def main(argv=None):
     ap.add_argument("--conv", choices=["c", "matlab"], default="c")
     ap.add_argument("--payload", choices=["random", "message", "tester"])
     ap.add_argument("--message", help="MESSAGE payload text (default: OFDM.c:20), up to 96 characters")
+    ap.add_argument("--evm", choices=["trial", "pooled"], default="trial",
+                    help="EVM files: mean of per-trial EVM_dB (the reference's per-trial value) or pooled")
     ap.add_argument("--print-messages", action="store_true",
                     help="as OFDM.c:1167-1182: receive one capture per SNR point and print the decoded text")
     a = ap.parse_args(argv)
     snr = np.array(a.snr) if a.snr else REF_SNR
     res = reference_main(a.out, a.trials, a.mode, snr, a.seed, est=a.est, noise=a.noise, channel=a.channel,
-                         conv=a.conv, payload=a.payload, message=a.message)
+                         conv=a.conv, payload=a.payload, message=a.message, evm=a.evm)
     for s, b, e in zip(res.snr_db, res.ber, res.evm_pre_db):
         print(f"SNR = {s:5.1f} dB   BER = {b:.3e}   EVM = {e:7.2f} dB", file=sys.stderr)
     if a.print_messages:

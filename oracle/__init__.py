@@ -9,4 +9,4 @@ The product library (``ieee-802.11-ofdm-qpsk-simulator_amd``) never imports it.
 Parity of the restatement is pinned against the compiled reference and against
 ``data/Matlab_Output.txt`` (see tests/test_oracle.py and tests/golden/).
 """
-from .orc import Oracle, RefLib, ORACLE_DIR, build_oracle, build_ref  # noqa: F401
+from .orc import Oracle, RefLib, ORACLE_DIR, REF_SO, build_oracle, build_ref  # noqa: F401

@@ -239,6 +239,8 @@ class RefLib:
         L.ref_trial.argtypes = [C.c_float, C.c_void_p]
         L.ref_seed.argtypes = [C.c_uint64]
         L.ref_packet_selection.restype = C.c_int
+        L.ref_time_symbol_chain.restype = C.c_double
+        L.ref_time_symbol_chain.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
         self.n = L.ref_init()
 
     def waveform(self) -> np.ndarray:
@@ -309,4 +311,13 @@ class RefLib:
         acc = np.zeros(3, np.float64)
         self.lib.ref_seed(C.c_uint64(seed))
         t = self.lib.ref_time_trials(C.c_float(snr_db), int(n_trials), _p(acc))
+        return t, acc
+
+    def time_symbol_chain(self, snr_db, n_frames: int, rayleigh: bool = False, seed: int = 0x80211A):
+        """The genie symbol chain of the GPU sweep built from the reference's own stage functions
+        (ref_harness.c ref_time_symbol_chain); returns (seconds, [bit errors, bits, sum|z-d|^2])."""
+        snr = np.ascontiguousarray(snr_db, np.float32)
+        acc = np.zeros(3, np.float64)
+        self.lib.ref_seed(C.c_uint64(seed))
+        t = self.lib.ref_time_symbol_chain(_p(snr), len(snr), int(n_frames), int(rayleigh), _p(acc))
         return t, acc

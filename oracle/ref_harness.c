@@ -342,3 +342,115 @@ void ref_gaussian_noise(int n, float *out)
 {
     for (int i = 0; i < n; ++i) out[i] = gaussian_noise(0, 1);
 }
+
+/*
+ * CPU baseline for the symbol-mode workloads (bench.py cpu_baseline, configs c2/c3/c4/c5): the
+ * genie-timed symbol chain of the GPU sweep composed from the reference's OWN stage functions,
+ * timed on this host.  Per frame the Tx is built once (QPSK_Modulator OFDM.c:415-433, subcarrier
+ * map as Transmitter OFDM.c:523-548, ifft OFDM.c:320-339, CP OFDM.c:559-565) and re-used for every
+ * SNR point, as the GPU sweep re-uses its Tx batch.  Per SNR point: real-only noise from the
+ * reference's gaussian_noise (OFDM.c:622-632, 651) on the samples the receiver reads (LTF pair +
+ * 2 data windows), Channel_Estimation (OFDM.c:830-850), fft + ZF + demap (Receiver's inline loops
+ * OFDM.c:1024-1069, restated), AGC_Receiver (852-871), QPSK_Demodulator (873-908), EVM and BER
+ * sums (1104-1161, restated).  Noise var = kappa P_ref / 10^(snr/10).
+ * rayleigh = 1 (config c5, no reference counterpart, D9): a 4-tap CN(0, 1/4) channel per frame
+ * (restated) and complex noise of the same total variance, kappa = 1.
+ * acc3 += {bit errors, bits, sum |z - d|^2}.  Returns wall seconds.
+ */
+static unsigned long long g_bits_state = 0x9E3779B97F4A7C15ULL;
+static unsigned int bits_next(void)
+{
+    g_bits_state ^= g_bits_state << 13; g_bits_state ^= g_bits_state >> 7; g_bits_state ^= g_bits_state << 17;
+    return (unsigned int)(g_bits_state >> 11);
+}
+
+double ref_time_symbol_chain(const float *snr_db, int n_snr, int n_frames, int rayleigh, double *acc3)
+{
+    ref_init();
+    const int D = data_frames_number;     /* 2 for the reference message (OFDM.c:439) */
+    const int pilot[4] = {1, 1, 1, -1};
+    float complex T[64], ltf[64];
+    memcpy(ltf, Long_preamble_slot_Frequency, sizeof(ltf));
+    ifft(ltf, T, 64);                                      /* long training symbol, C ifft (D5) */
+    float complex **payload = Allocate_Array_2D(D, 96), **mod = Allocate_Array_2D(D, 48);
+    float complex frame_tx[480], frame_rx[480], H[64];
+    float complex **rx_time = Allocate_Array_2D(D, 64), **rx_freq = Allocate_Array_2D(D, 64);
+    float complex **no_pilot = Allocate_Array_2D(D, 48), **final = Allocate_Array_2D(D, 48);
+    float complex **demod = Allocate_Array_2D(D, 96);
+    double be = 0, nb = 0, epre = 0;
+    struct timespec t0, t1;
+    quiet_begin();
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int f = 0; f < n_frames; ++f) {
+        memset(frame_tx, 0, sizeof(frame_tx));
+        for (int i = 0; i < 64; ++i) { frame_tx[192 + i] = T[i]; frame_tx[256 + i] = T[i]; }
+        for (int d = 0; d < D; ++d) {
+            for (int j = 0; j < 96; j += 32) {
+                unsigned int w = bits_next();
+                for (int b = 0; b < 32; ++b) payload[d][j + b] = (w >> (31 - b)) & 1u;
+            }
+        }
+        QPSK_Modulator(payload, mod, D);
+        for (int d = 0; d < D; ++d) {
+            float complex X[64] = {0}, x[64];
+            Slice_Repeater(mod[d], X, 6, 0, 5, 1);   X[11] = pilot[0];
+            Slice_Repeater(mod[d], X, 12, 5, 18, 1); X[25] = pilot[1];
+            Slice_Repeater(mod[d], X, 26, 18, 24, 1);
+            Slice_Repeater(mod[d], X, 33, 24, 30, 1); X[39] = pilot[2];
+            Slice_Repeater(mod[d], X, 40, 30, 43, 1); X[53] = pilot[3];
+            Slice_Repeater(mod[d], X, 54, 43, 48, 1);
+            ifft(X, x, 64);
+            Slice_Repeater(x, frame_tx, 320 + 80 * d, 48, 64, 1);
+            Slice_Repeater(x, frame_tx, 336 + 80 * d, 0, 64, 1);
+        }
+        if (rayleigh) {          /* y[n] = sum_l h_l x[n - l], taps CN(0, 1/4) (Box-Muller on rand()) */
+            float complex h[4], y[480];
+            for (int l = 0; l < 4; ++l) h[l] = 0.5f * (gaussian_noise(0, 0.5f) + I * gaussian_noise(0, 0.5f));
+            for (int n = 0; n < 480; ++n) {
+                y[n] = 0;
+                for (int l = 0; l < 4 && l <= n; ++l) y[n] += h[l] * frame_tx[n - l];
+            }
+            memcpy(frame_tx, y, sizeof(y));
+        }
+        for (int q = 0; q < n_snr; ++q) {
+            const float kappa = rayleigh ? 1.0f : 0.4980f;
+            const float sd = sqrtf(kappa * 52.0f / 4096.0f / powf(10.0f, snr_db[q] / 10.0f));
+            const float sc = rayleigh ? sd * 0.70710678f : sd;
+            memcpy(frame_rx, frame_tx, sizeof(frame_rx));
+            for (int i = 192; i < 320; ++i)
+                frame_rx[i] += rayleigh ? sc * (gaussian_noise(0, 1) + I * gaussian_noise(0, 1)) : sd * gaussian_noise(0, 1);
+            for (int d = 0; d < D; ++d)
+                for (int i = 336 + 80 * d; i < 400 + 80 * d; ++i)
+                    frame_rx[i] += rayleigh ? sc * (gaussian_noise(0, 1) + I * gaussian_noise(0, 1))
+                                            : sd * gaussian_noise(0, 1);
+            Channel_Estimation(frame_rx, H, 480);
+            for (int d = 0; d < D; ++d) {
+                Slice_Repeater(frame_rx, rx_time[d], 0, 336 + 80 * d, 400 + 80 * d, 1);
+                fft(rx_time[d], rx_freq[d], 64);
+                for (int j = 0; j < 64; ++j) rx_freq[d][j] = rx_freq[d][j] / H[j];
+                Slice_Repeater(rx_freq[d], no_pilot[d], 0, 6, 11, 1);
+                Slice_Repeater(rx_freq[d], no_pilot[d], 5, 12, 25, 1);
+                Slice_Repeater(rx_freq[d], no_pilot[d], 18, 26, 32, 1);
+                Slice_Repeater(rx_freq[d], no_pilot[d], 24, 33, 39, 1);
+                Slice_Repeater(rx_freq[d], no_pilot[d], 30, 40, 53, 1);
+                Slice_Repeater(rx_freq[d], no_pilot[d], 43, 54, 59, 1);
+            }
+            AGC_Receiver(no_pilot, final);
+            QPSK_Demodulator(final, demod, D);
+            float es = 0;
+            for (int d = 0; d < D; ++d)
+                for (int j = 0; j < 48; ++j) es += pow(cabs(no_pilot[d][j] - mod[d][j]), 2);
+            float sum = 0;
+            for (int d = 0; d < D; ++d)
+                for (int j = 0; j < 96; ++j) sum += abs(creal(payload[d][j]) - creal(demod[d][j]));
+            be += sum; nb += 96 * D; epre += es;
+        }
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    quiet_end();
+    Deallocate_Array_2D(payload, D); Deallocate_Array_2D(mod, D);
+    Deallocate_Array_2D(rx_time, D); Deallocate_Array_2D(rx_freq, D);
+    Deallocate_Array_2D(no_pilot, D); Deallocate_Array_2D(final, D); Deallocate_Array_2D(demod, D);
+    if (acc3) { acc3[0] += be; acc3[1] += nb; acc3[2] += epre; }
+    return (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
+}

@@ -1,0 +1,132 @@
+"""Multi-rank paths through the HIP library (BASELINE configs[3] C4 / configs[4] C5).
+
+* C4's per-rank shard at its stated size (1e8 symbols/point over 8 ranks = 1.25e7 per rank) equals
+  the sum of its two halves bit for bit (counter-range sharding of OFDM.c's trial loop :1195-1222).
+* Two spawned processes on cuda:0 run Engine.symbol_sweep / sweep.reference_main on their shard
+  and reduce through dist.allreduce_counters over gloo: bit-identical to one process.
+* torchrun launches bench.py as a fresh child, so init_process_group("nccl") and the RCCL
+  all-reduce of the counters run on the MI355X.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+SNR = np.arange(0.0, 31.0, 2.0)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_c4_rank_shard_equals_halves(engine, pkg):
+    """C4: 1e8 symbols/point on 8 GPUs -> one rank's 1.25e7 symbols/point (6.25e6 frames), here rank 3."""
+    from ofdm_amd import dist as odist
+    frames_total = 100_000_000 // 2
+    a, b = odist.shard_range(frames_total, 3, 8)
+    assert b - a == 6_250_000
+    cfg = pkg.make_cfg()
+    whole = engine.symbol_sweep(cfg, SNR, b - a, first_frame=a)
+    m = (a + b) // 2
+    halves = engine.symbol_sweep(cfg, SNR, m - a, first_frame=a) + engine.symbol_sweep(cfg, SNR, b - m, first_frame=m)
+    assert np.array_equal(whole, halves)
+    assert np.all(whole[:, 0] == b - a) and np.all(whole[:, 2] == 192 * (b - a))
+    # a different chunking of the same range
+    assert np.array_equal(whole, engine.symbol_sweep(cfg, SNR, b - a, first_frame=a, chunk_frames=1_000_003))
+
+
+def test_c5_rank_shard_equals_halves(engine, pkg):
+    """C5: 1e9 symbol-SNR evaluations on 8 GPUs -> 3.90625e6 frames per rank (4-tap Rayleigh, complex AWGN)."""
+    from ofdm_amd import dist as odist
+    frames_total = 1_000_000_000 // 16 // 2
+    a, b = odist.shard_range(frames_total, 5, 8)
+    cfg = pkg.make_cfg(noise="complex", channel="rayleigh4", kappa=1.0)
+    whole = engine.symbol_sweep(cfg, SNR, b - a, first_frame=a)
+    m = a + 1_234_567
+    halves = engine.symbol_sweep(cfg, SNR, m - a, first_frame=a) + engine.symbol_sweep(cfg, SNR, b - m, first_frame=m)
+    assert np.array_equal(whole, halves)
+    ber = whole[:, 3] / whole[:, 2]
+    assert np.all(np.diff(ber[:8]) < 0)                 # BER falls with SNR (diversity-limited slope)
+
+
+def _sweep_worker(rank, world, port, n, out_path):
+    sys.path.insert(0, str(ROOT))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0", OFDM_DIST_BACKEND="gloo")
+    import ofdm_pkg
+    pkg = ofdm_pkg.load()
+    from ofdm_amd import dist as odist
+    assert odist.init_from_env()
+    import torch.distributed as dist
+    with pkg.Engine(0) as eng:
+        a, b = odist.shard_range(n, rank, world)
+        c = eng.symbol_sweep(pkg.make_cfg(), SNR, b - a, first_frame=a)
+    c = odist.allreduce_counters_np(c)
+    if rank == 0:
+        np.save(out_path, c)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_ranks_hip_symbol_sweep_equals_single(engine, pkg, tmp_path):
+    n = 300_001
+    out = tmp_path / "c.npy"
+    mp.spawn(_sweep_worker, args=(2, _free_port(), n, str(out)), nprocs=2, join=True)
+    got = np.load(out)
+    assert np.array_equal(got, engine.symbol_sweep(pkg.make_cfg(), SNR, n))
+
+
+def _main_worker(rank, world, port, out_dir):
+    sys.path.insert(0, str(ROOT))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0", OFDM_DIST_BACKEND="gloo")
+    import ofdm_pkg
+    ofdm_pkg.load()
+    from ofdm_amd import sweep
+    import torch.distributed as dist
+    sweep.reference_main(out_dir, trials=5001, snr_db=[6.0, 8.0, 10.0, 20.0])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_ranks_reference_main_equals_single(pkg, tmp_path):
+    """reference_main under torchrun forms the group itself and rank 0 writes the reduced
+    files -- identical to the single-process files (frame mode: trials split by counter range)."""
+    from ofdm_amd import sweep
+    d2, d1 = tmp_path / "two", tmp_path / "one"
+    d2.mkdir(); d1.mkdir()
+    mp.spawn(_main_worker, args=(2, _free_port(), str(d2)), nprocs=2, join=True)
+    sweep.reference_main(d1, trials=5001, snr_db=[6.0, 8.0, 10.0, 20.0])
+    for name in ("Output_SNR.txt", "Output_EVM_AGC.txt", "Output_EVM_AGC_DB.txt", "Output_BER.txt"):
+        assert (d2 / name).read_text() == (d1 / name).read_text(), name
+    c2 = json.loads((d2 / "ofdm_sweep.json").read_text())
+    c1 = json.loads((d1 / "ofdm_sweep.json").read_text())
+    assert c2["counters"] == c1["counters"] and c2["world"] == 2
+
+
+@pytest.mark.parametrize("workload,symbols", [("c3", 200_000), ("c4", 400_000)])
+def test_torchrun_bench_rccl(workload, symbols):
+    """bench.py under torch.distributed.run (one rank): init_process_group("nccl") + the RCCL
+    all-reduce of the counters execute on the GPU; the JSON line is well formed."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(ROOT / "bench.py"), "--gpus", "1",
+           "--workload", workload, "--symbols", str(symbols), "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+    env = dict(os.environ, PYTHONUNBUFFERED="1")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=str(ROOT))
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 1 and line["value"] > 0
+    assert "RCCL all-reduce" in line["config"]["parallelism"]
+    assert line["results"]["frames_per_snr"] == symbols // 2
+    assert line["scaling"] == ("weak" if workload == "c3" else "strong")

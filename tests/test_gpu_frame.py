@@ -107,6 +107,93 @@ def test_frame_sweep_vs_oracle(engine, oracle, pkg):
     assert np.all(np.abs(g[:, 5] - o[:, 5]) <= np.sum(gp != op, axis=1))
 
 
+def _drop_trials(sweep, snrs, trials, n_counters=16):
+    """counters of the given trials (one call each, same SNR grid, so the same streams)"""
+    acc = np.zeros((len(snrs), n_counters), np.int64)
+    for t in trials:
+        acc += sweep(int(t))
+    return acc
+
+
+def test_frame_sweep_evm_counters_vs_oracle(engine, oracle, pkg):
+    """The counters behind Output_EVM_AGC.txt / Output_EVM_AGC_DB.txt (OFDM.c:1104-1150, 1228-1231):
+    EVM_PRE_Q (7), EVM_POST_AXIS (8), EVMDB_PRE_Q (9), EVMDB_POST_Q (10), EVMDB_POST_FINITE (11) of
+    the batched sweep (frame_sym_kernel<false>) vs the oracle on the same Philox streams.  Trials
+    whose packet_idx differs (fp32 vs double at the 0.75 threshold) are re-run one by one on both
+    sides and subtracted, so the remaining trials are compared tightly."""
+    snrs = [0.0, 3.0, 6.0, 8.0, 10.0, 14.0, 30.0]
+    n = 400
+    cfg_g, cfg_o = pkg.make_cfg(payload="message"), oracle.cfg(payload="message")
+    g, gp = engine.frame_sweep(cfg_g, snrs, n, want_packet_idx=True)
+    o, op = oracle.frame_sweep(cfg_o, snrs, 0, n, "c", dump_pidx=True)
+    bad = np.nonzero(np.any(gp != op, axis=0))[0]
+    assert len(bad) <= 0.01 * n * len(snrs), len(bad)
+    g = g - _drop_trials(lambda t: engine.frame_sweep(cfg_g, snrs, 1, first_trial=t), snrs, bad)
+    o = o - _drop_trials(lambda t: oracle.frame_sweep(cfg_o, snrs, t, 1, "c"), snrs, bad)
+    nf = g[:, 0]
+    assert np.array_equal(nf, o[:, 0]) and np.all(nf == n - len(bad))
+    assert np.array_equal(g[:, 5], o[:, 5])                                   # sync failures
+    q = 2.0 ** 20
+    # before the slicer: per-frame sum |z - d|^2 (fp32 vs double) and per-frame EVM_dB
+    assert np.all(np.abs(g[:, 7] - o[:, 7]) <= 2e-5 * o[:, 7] + nf), (g[:, 7], o[:, 7])
+    assert np.all(np.abs(g[:, 9] - o[:, 9]) / q <= 1e-3 * nf), (g[:, 9] / q / nf, o[:, 9] / q / nf)
+    # after the slicer: axis errors and finite-frame counts exact up to near-threshold decisions
+    d8, d11 = np.abs(g[:, 8] - o[:, 8]), np.abs(g[:, 11] - o[:, 11])
+    assert np.all(d8 <= 2) and np.all(d11 <= 1), (g[:, 8], o[:, 8], g[:, 11], o[:, 11])
+    assert np.all(np.abs(g[:, 10] - o[:, 10]) / q <= 1e-3 * nf + 25.0 * (d8 + d11))
+    # the regimes are all present: sync failures, slicer errors in every frame, none at all
+    assert o[0, 5] > 0 and o[0, 11] == nf[0] and o[-1, 11] == 0 and o[-1, 8] == 0
+
+
+def _curve_rows():
+    return json.loads((GOLDEN / "ref_mc_curve.json").read_text())["rows"]
+
+
+def _evm_batches(engine, pkg, snr, batches, per_batch):
+    """per-batch mean per-trial EVM_dB before / after the slicer, and finite post-slicer counts"""
+    cfg = pkg.make_cfg(payload="message")
+    pre, post, fin, frames = [], [], [], []
+    for b in range(batches):
+        c = engine.frame_sweep(cfg, snr, per_batch, first_trial=b * per_batch)
+        pre.append(c[:, 9] / 2.0 ** 20 / c[:, 0])
+        post.append(c[:, 10] / 2.0 ** 20 / np.maximum(c[:, 11], 1))
+        fin.append(c[:, 11]); frames.append(c[:, 0])
+    return np.array(pre), np.array(post), np.sum(fin, axis=0), np.sum(frames, axis=0)
+
+
+def test_reference_evm_curve(engine, pkg):
+    """configs[2] "reproduce Output_EVM_AGC.txt": the mean per-trial EVM_dB of the GPU frame sweep
+    vs the compiled reference's own trial loop (ref_mc_curve.json, 48000 trials/point), before the
+    slicer at every point 0..30 dB and after it where the reference mean is finite (0..2 dB: every
+    trial has slicer errors) or -inf (3..30 dB: some trial has none, OFDM.c:1148-1150).  Bound: 5
+    standard errors of the difference (GPU batch spread, reference scaled by its trial count) plus
+    0.03 dB for the RNG difference (glibc-style rand() Box-Muller vs Philox, D8)."""
+    rows = _curve_rows()
+    snr = np.array([r["snr_db"] for r in rows])
+    K, B = 16, 25_000
+    pre_b, post_b, fin, frames = _evm_batches(engine, pkg, snr, K, B)
+    for i, r in enumerate(rows):
+        m = pre_b[:, i].mean()
+        se = pre_b[:, i].std(ddof=1) / np.sqrt(K)
+        se_ref = pre_b[:, i].std(ddof=1) * np.sqrt(B / r["trials"])
+        tol = 5 * np.hypot(se, se_ref) + 0.03
+        print(f"{r['snr_db']:5.1f} dB  EVM pre: GPU {m:8.3f}  reference {r['mean_evm_db']:8.3f}  "
+              f"diff {m - r['mean_evm_db']:+.3f}  tol {tol:.3f}")
+        assert abs(m - r["mean_evm_db"]) < tol, (r["snr_db"], m, r["mean_evm_db"], tol)
+        ref_post = r["mean_evm_agc_db"]
+        # trials without any slicer error make the reference's mean -inf: expected count in its sample
+        lam = (frames[i] - fin[i]) / frames[i] * r["trials"]
+        if np.isfinite(ref_post):
+            assert lam < 5, (r["snr_db"], lam)             # P(none of 48000 | lam >= 5) < 0.7 %
+            mp = post_b[:, i].mean()
+            sp = post_b[:, i].std(ddof=1)
+            tolp = 5 * np.hypot(sp / np.sqrt(K), sp * np.sqrt(B / r["trials"])) + 0.03
+            print(f"{r['snr_db']:5.1f} dB  EVM post: GPU {mp:8.3f}  reference {ref_post:8.3f}  tol {tolp:.3f}")
+            assert abs(mp - ref_post) < tolp, (r["snr_db"], mp, ref_post)
+        else:
+            assert lam > 0.01, (r["snr_db"], lam)          # P(at least one of 48000 | lam <= 0.01) < 1 %
+
+
 def test_frame_sweep_noiseless_and_edges(engine, pkg):
     cfg = pkg.make_cfg(payload="message", noise="none")
     c, p = engine.frame_sweep(cfg, [20.0], 2000, want_packet_idx=True)
@@ -164,6 +251,34 @@ def test_reference_ber_curve_within_tenth_db(engine, pkg):
     for s, b, r, n in zip(snr, ber, ref, n_ref):
         sd = math.sqrt(max(r, 1e-4) * 0.5 / n + max(b, 1e-4) * 0.5 / 200_000)
         assert abs(b - r) < 6 * sd + 2e-4, (s, b, r)
+
+
+def test_reference_main_evm_files_vs_reference_curve(pkg, tmp_path):
+    """main()'s EVM files at SNR 6..40 (OFDM.c:1195-1231) with 100k trials per point vs the reference
+    curve: Output_EVM_AGC.txt (mean per-trial EVM_dB before the slicer) within the fixture's sampling
+    error + the "%.2e" rounding of the file; Output_EVM_AGC_DB.txt -inf wherever the reference's
+    mean is -inf (3..30 dB)."""
+    from ofdm_amd import sweep
+    sweep.reference_main(tmp_path, trials=100_000)
+    snr = pkg.read_float_array_file(tmp_path / "Output_SNR.txt")
+    pre = pkg.read_float_array_file(tmp_path / "Output_EVM_AGC.txt")
+    post = pkg.read_float_array_file(tmp_path / "Output_EVM_AGC_DB.txt")
+    side = json.loads((tmp_path / "ofdm_sweep.json").read_text())
+    assert side["evm_files"] == "trial"
+    curve = {r["snr_db"]: r for r in _curve_rows()}
+    hits = 0
+    for s, e, ep, exact in zip(snr, pre, post, side["mean_trial_evm_db"]):
+        assert e == float("%.2e" % np.float32(exact))
+        if s in curve:
+            hits += 1
+            r = curve[s]
+            ulp = 0.5 * 10 ** (np.floor(np.log10(abs(r["mean_evm_db"]))) - 2)
+            sd_trial = 10.0 if s <= 12 else 1.0      # per-trial EVM_dB spread (sync failures below 13 dB)
+            tol = 5 * sd_trial * np.sqrt(1 / 100_000 + 1 / r["trials"]) + 0.03
+            assert abs(e - r["mean_evm_db"]) < tol + ulp, (s, e, r["mean_evm_db"])
+            assert np.isneginf(ep) and np.isneginf(r["mean_evm_agc_db"])
+    assert hits == 18
+    assert np.all(np.isneginf(post))
 
 
 def test_reference_main_writes_files(pkg, tmp_path):

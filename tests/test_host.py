@@ -111,3 +111,44 @@ def test_shard_ranges(pkg):
             rs = [dist.shard_range(n, r, w) for r in range(w)]
             assert rs[0][0] == 0 and rs[-1][1] == n
             assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
+
+
+def test_allreduce_refuses_world_without_group(pkg, monkeypatch):
+    """a sharded sweep must never be written from one rank's share: with WORLD_SIZE > 1
+    and no process group the reduction raises instead of silently returning."""
+    import torch
+    from ofdm_amd import dist as odist
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    with pytest.raises(odist.DistError):
+        odist.allreduce_counters(torch.zeros((2, 16), dtype=torch.int64))
+    with pytest.raises(odist.DistError):
+        odist.allreduce_counters_np(np.zeros((2, 16), np.int64))
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    c = np.arange(32, dtype=np.int64).reshape(2, 16)
+    assert odist.allreduce_counters_np(c) is c
+
+
+def test_mean_trial_evm_semantics(pkg):
+    """Output_EVM_AGC*.txt values for trials > 1: mean of the per-trial EVM_dB; the post-slicer mean
+    is -inf once any trial had no slicer error (that trial's own value is -inf, OFDM.c:1148-1150)."""
+    from ofdm_amd import abi
+    c = np.zeros((2, 16), np.int64)
+    c[:, abi.C_FRAMES] = 4
+    c[:, abi.C_EVMDB_PRE_Q] = [-40 << 20, 8 << 20]
+    c[:, abi.C_EVMDB_POST_Q] = [0, 6 << 20]
+    c[:, abi.C_EVMDB_POST_FINITE] = [0, 4]
+    r = pkg.SweepResult(np.array([30.0, 0.0]), c)
+    assert list(r.mean_frame_evm_db) == [-10.0, 2.0]
+    assert np.isneginf(r.mean_frame_evm_post_db[0]) and r.mean_frame_evm_post_db[1] == 1.5
+
+
+def test_reference_symbol_chain_baseline_is_the_genie_workload(reflib):
+    """bench.py's cpu_baseline for c2-c5 runs the reference's own stage functions as the genie symbol
+    chain (ref_harness.c ref_time_symbol_chain): its BER at 0 / 4 dB is the genie fixture's."""
+    rows = {r["snr_db"]: r for r in json.loads((GOLDEN / "ref_genie_ls_curve.json").read_text())["rows"]}
+    for snr, n in ((0.0, 3000), (4.0, 6000)):
+        t, acc = reflib.time_symbol_chain([snr], n)
+        ber, ref = acc[0] / acc[1], rows[snr]["bit_err"] / rows[snr]["bits"]
+        sd = np.sqrt(ref / acc[1] + ref / rows[snr]["bits"]) * 3      # ~3 bit errors per error event
+        assert abs(ber - ref) < 5 * sd, (snr, ber, ref)
+        assert t > 0

@@ -1,25 +1,29 @@
 """Summarise rocprofv3 --kernel-trace / --pmc runs (tools/gpu_profile.sh) into profiles/.
 
-usage: python tools/pmc_summary.py <gpurun_out dir> <workload> <units_per_launch> [--out profiles/pmc_summary.json]
+usage: python tools/pmc_summary.py <gpurun_out dir> <workload> <units_total_in_run> [--out FILE]
 
-Per receiver launch (mean over the dispatches of the run):
+<units_total_in_run>: symbol-SNR evaluations the profiled command processed in ALL its receiver
+dispatches (warmup steps included), e.g. (warmup + steps) x symbols x 16 SNR points.
+
+Counters are summed over every dispatch of the workload's receiver kernels (symbol mode:
+rx_ls_kernel / rx_ideal_kernel; frame mode: frame_sync_kernel + frame_sym_kernel, which the frame
+timer brackets together) and divided by the units:
   * HBM bytes: FETCH_SIZE (KB) x 1024 x 2 -- gfx950 reports half of the bytes of wide (16 B/lane)
     coalesced streaming reads, LDS-DMA included (MI355X_MICROARCH.md, HBM section) -- plus
     WRITE_SIZE (KB) x 1024;
-  * VALU: SQ_INSTS_VALU wave-instructions per launch and per second against the issue peak
-    (256 CUs x 4 SIMDs x 1 wave-instruction / 2 cycles, tools/ubench_valu.hip) at the clock
+  * VALU: SQ_INSTS_VALU wave-instructions per unit, and the issue rate against the peak
+    (256 CUs x 4 SIMDs x 1 wave-instruction / 2 cycles) at 2.4 GHz and at the clock
     GRBM_GUI_ACTIVE / duration shows.
 """
 import csv
 import json
-import statistics
 import sys
 from collections import defaultdict
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 KERNELS = ("rx_ls_kernel", "rx_ideal_kernel", "tx_symbols_kernel", "frame_sync_kernel", "frame_sym_kernel")
-BYTES_PER_UNIT = 652
+RX_SETS = (("rx_ls_kernel",), ("rx_ideal_kernel",), ("frame_sync_kernel", "frame_sym_kernel"))
 CUS, SIMDS, XCDS = 256, 4, 8
 NOMINAL_CLOCK = 2.4e9
 
@@ -32,17 +36,17 @@ def kernel_key(name):
 
 
 def read_counters(d: Path):
-    vals = defaultdict(lambda: defaultdict(list))      # kernel -> counter -> [per dispatch]
-    durs = defaultdict(list)
+    sums = defaultdict(lambda: defaultdict(float))     # kernel -> counter -> sum over dispatches
+    n = defaultdict(lambda: defaultdict(int))
     for f in sorted(d.glob("pmc_*/**/*counter_collection.csv")):
         with open(f) as fh:
             for r in csv.DictReader(fh):
                 k = kernel_key(r["Kernel_Name"])
                 if not k:
                     continue
-                vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
-                durs[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
-    return vals, durs
+                sums[k][r["Counter_Name"]] += float(r["Counter_Value"])
+                n[k][r["Counter_Name"]] += 1
+    return sums, n
 
 
 def read_trace(d: Path):
@@ -52,47 +56,46 @@ def read_trace(d: Path):
             for r in csv.DictReader(fh):
                 k = kernel_key(r["Name"])
                 if k:
-                    out[k] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"])}
+                    out[k] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
+                              "total_ns": float(r["TotalDurationNs"])}
     return out
 
 
 def main(argv):
     d, workload, units = Path(argv[0]), argv[1], float(argv[2])
     out = Path(argv[argv.index("--out") + 1]) if "--out" in argv else ROOT / "profiles" / "pmc_summary.json"
-    vals, _ = read_counters(d)
+    sums, ndisp = read_counters(d)
     trace = read_trace(d)
     summary = json.loads(out.read_text()) if out.exists() else {}
-    # the receiver kernel of this run (symbol-mode LS / ideal, or frame mode)
-    rx = next(k for k in ("rx_ls_kernel", "rx_ideal_kernel", "frame_sync_kernel") if k in vals)
-    c = {k: statistics.mean(v) for k, v in vals[rx].items()}
-    t = trace.get(rx, {}).get("avg_ns", float("nan")) * 1e-9
+    rx = next(s for s in RX_SETS if s[0] in sums)
+    c = defaultdict(float)
+    for k in rx:
+        for name, v in sums[k].items():
+            c[name] += v
+    t_total = sum(trace.get(k, {}).get("total_ns", 0.0) for k in rx) * 1e-9
     rd = 2.0 * c.get("FETCH_SIZE", float("nan")) * 1024
     wr = c.get("WRITE_SIZE", float("nan")) * 1024
-    # GRBM_GUI_ACTIVE is summed over the 8 XCDs
-    clk = c.get("GRBM_GUI_ACTIVE", float("nan")) / XCDS / t if t == t else float("nan")
+    clk = c.get("GRBM_GUI_ACTIVE", float("nan")) / XCDS / t_total if t_total else float("nan")
     valu = c.get("SQ_INSTS_VALU", float("nan"))
-    peak_valu = CUS * SIMDS * 0.5 * NOMINAL_CLOCK      # 1 wave64 VALU instruction / 2 cycles / SIMD
+    peak = CUS * SIMDS * 0.5 * NOMINAL_CLOCK
     entry = {
-        "kernel": rx,
-        "units_per_launch": units,
-        "avg_launch_ms_trace": t * 1e3,
-        "algorithmic_bytes_per_launch": BYTES_PER_UNIT * units,
-        "fetch_size_kb_raw": c.get("FETCH_SIZE"),
-        "write_size_kb_raw": c.get("WRITE_SIZE"),
-        "rx_hbm_read_bytes_per_launch": rd,
-        "rx_hbm_write_bytes_per_launch": wr,
-        "rx_hbm_bytes_per_launch": rd + wr,
-        "hbm_gbs_measured": (rd + wr) / t / 1e9,
+        "kernels": list(rx),
+        "units_total_in_run": units,
+        "kernel_time_s_trace": t_total,
+        "hbm_read_bytes_per_unit": rd / units,
+        "hbm_write_bytes_per_unit": wr / units,
+        "hbm_bytes_per_unit": (rd + wr) / units,
+        "hbm_gbs_measured": (rd + wr) / t_total / 1e9 if t_total else None,
         "clock_ghz": clk / 1e9,
-        "valu_instr_per_launch": valu,
         "valu_instr_per_unit": valu / units,
-        "valu_instr_per_s": valu / t,
-        "valu_issue_peak_per_s": peak_valu,
-        "valu_frac": valu / t / peak_valu,
-        "valu_frac_at_measured_clock": valu / t / (CUS * SIMDS * 0.5 * clk),
-        "counters_mean_per_launch": c,
+        "valu_instr_per_s": valu / t_total if t_total else None,
+        "valu_issue_peak_per_s": peak,
+        "valu_frac": valu / t_total / peak if t_total else None,
+        "valu_frac_at_measured_clock": valu / t_total / (CUS * SIMDS * 0.5 * clk) if t_total else None,
+        "counters_sum_per_unit": {k: v / units for k, v in c.items()},
+        "dispatches_per_counter": {k: dict(v) for k, v in ndisp.items() if k in rx},
         "trace": trace,
-        "note": "FETCH_SIZE doubled (gfx950 reports half of wide streaming reads); per-dispatch means",
+        "note": "FETCH_SIZE doubled (gfx950 reports half of wide streaming reads); sums over dispatches / units",
     }
     summary[workload] = entry
     out.write_text(json.dumps(summary, indent=1, sort_keys=True))
