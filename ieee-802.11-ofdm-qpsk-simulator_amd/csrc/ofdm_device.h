@@ -24,6 +24,12 @@ __device__ __forceinline__ void static_for(F &&f) {
     }
 }
 
+// Hide a value from the optimiser for one program point.  Used inside the per-SNR loop so that
+// loop-invariant work (64 load addresses, 96 truth-symbol selects, the first Philox round) is
+// recomputed each iteration instead of being hoisted and held in ~200 extra VGPRs.
+template <typename T>
+__device__ __forceinline__ void opaque(T &v) { asm volatile("" : "+v"(v)); }
+
 // ------------------------------------------------------------------ complex helpers
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
@@ -83,6 +89,40 @@ __device__ __forceinline__ uint4 philox10_c2(const PhiloxHead &h, uint32_t c2, u
         k0 += PHILOX_W0; k1 += PHILOX_W1;
     }
     return make_uint4(c0, c1, c2, c3);
+}
+
+// philox10_c2 for NB blocks at once (same outputs), round keys in VGPRs: a v_bitop3_b32 with an SGPR
+// operand issues at the slow rate, one with three VGPRs at the fast rate.  The keys
+// are moved to VGPRs once and advanced round by round with v_add (literal W0 / W1), shared by the NB
+// blocks; opaque() keeps the nine round keys from being formed up front (2 live VGPRs, not 18).
+template <int NB>
+__device__ __forceinline__ void philox10_c2_vk(const PhiloxHead &h, const uint32_t (&c2in)[NB], uint32_t k0,
+                                               uint32_t k1, uint4 (&out)[NB]) {
+    uint32_t kv0, kv1;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(kv0) : "s"(k0));
+    asm volatile("v_mov_b32 %0, %1" : "=v"(kv1) : "s"(k1));
+    uint32_t c0[NB], c1[NB], c2[NB], c3[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const uint64_t p1r = (uint64_t)PHILOX_M1 * c2in[b];
+        c0[b] = __builtin_amdgcn_bitop3_b32((uint32_t)(p1r >> 32), h.c1, kv0, 0x96);
+        c1[b] = (uint32_t)p1r; c2[b] = h.n2; c3[b] = h.c3;
+    }
+#pragma unroll
+    for (int r = 1; r < 10; ++r) {
+        kv0 += PHILOX_W0; kv1 += PHILOX_W1;
+        opaque(kv0); opaque(kv1);
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            const uint64_t p0 = (uint64_t)PHILOX_M0 * c0[b];
+            const uint64_t p1 = (uint64_t)PHILOX_M1 * c2[b];
+            const uint32_t n0 = __builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c1[b], kv0, 0x96);
+            const uint32_t n2 = __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c3[b], kv1, 0x96);
+            c0[b] = n0; c1[b] = (uint32_t)p1; c2[b] = n2; c3[b] = (uint32_t)p0;
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) out[b] = make_uint4(c0[b], c1[b], c2[b], c3[b]);
 }
 
 // Box-Muller pair.  u1 = fma((float)x1, 2^-32, 2^-33) in (0, 1] (tail to 6.7 sigma);
@@ -195,12 +235,6 @@ __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0
 #else
 __device__ __forceinline__ void sched_fence() {}
 #endif
-
-// Hide a value from the optimiser for one program point.  Used inside the per-SNR loop so that
-// loop-invariant work (64 load addresses, 96 truth-symbol selects, the first Philox round) is
-// recomputed each iteration instead of being hoisted and held in ~200 extra VGPRs.
-template <typename T>
-__device__ __forceinline__ void opaque(T &v) { asm volatile("" : "+v"(v)); }
 
 // global-address-space views (keep loads global_* after opaque(), which erases provenance).
 // Native clang vectors, not float2 (HIP_vector_type's members are not address-space qualified).

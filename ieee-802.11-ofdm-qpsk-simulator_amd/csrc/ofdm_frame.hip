@@ -57,6 +57,7 @@ struct FrameArgs {
     int32_t fr_in_cap;              // fr[] inside the capture region (fr_in_capture)
     uint32_t k0, k1;
     uint32_t table[3 * FR_MAX_DATA];
+    uint32_t dtable[4 * FR_MAX_DATA];   // demap words of the payload symbols (ofdm_rxcommon.h)
     unsigned long long *counters;   // [n_snr][OFDM_NCOUNTERS]
     int32_t *pidx_out;              // [n_snr][n_trials] or null
     // per-trial debug outputs of item 0 (ofdm_receiver), all optional
@@ -684,7 +685,7 @@ __global__ __launch_bounds__(SYM_THREADS, FRAME_SYM_MINB) void frame_sym_kernel(
             static_for<0, 4>([&](auto ic) { dif_stage1<false, 4 * g + decltype(ic)::value>(x); });
             sched_fence();
         });
-        const uint32_t wd[3] = {a.table[3 * dsc], a.table[3 * dsc + 1], a.table[3 * dsc + 2]};
+        const uint32_t wd[4] = {a.dtable[4 * dsc], a.dtable[4 * dsc + 1], a.dtable[4 * dsc + 2], a.dtable[4 * dsc + 3]};
         SymState st;
         sym_init(st);
         const bool dump = DUMP && a.dbg_eq && item_ok && a.item0 + i == 0 && dlane;
@@ -693,7 +694,7 @@ __global__ __launch_bounds__(SYM_THREADS, FRAME_SYM_MINB) void frame_sym_kernel(
         static_for<0, 4>([&](auto rc) {
             constexpr int R = decltype(rc)::value;
             dif_sub16<false, R>(x);
-            demap_sub<DUMP, R, 2>(x, wd, Hof, deq, st);
+            demap_sub<DUMP, R, 2>(x, wd[R], Hof, deq, st);
             sched_fence();
         });
         if (role >= 2) {
@@ -835,6 +836,7 @@ static void fill_frame_args(FrameArgs &a, Ctx *c, const ofdm_rx_opts *o, int noi
     a.k0 = (uint32_t)seed;
     a.k1 = (uint32_t)(seed >> 32);
     a.n_data = payload_table(payload, c->message, a.table);
+    for (int d = 0; d < a.n_data; ++d) demap_words(a.table + 3 * d, a.dtable + 4 * d);
     a.word_stats = o->word_stats ? 1 : 0;
     rrc_taps(a.taps);
 }

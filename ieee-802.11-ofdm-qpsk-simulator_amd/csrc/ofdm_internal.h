@@ -13,7 +13,8 @@ constexpr int SYM_SAMPLES = 80;        // 64 + 16-sample cyclic prefix (OFDM.c:5
 
 // Tx batch layout, rows of symbols ("structure of arrays" over the batch):
 //   tx  [n * pitch + s] = time sample n (0..79, CP first) of data symbol s = 2 * frame + d
-//   bits[k * pitch + s] = payload word k (MSB-first bits 32k..32k+31) of symbol s
+//   bits[k * pitch + s] = payload word k (MSB-first bits 32k..32k+31) of symbol s, k = 0..2;
+//                         rows k = 3..6: demap word k - 3 (ofdm_rxcommon.h demap_word)
 // pitch = symbols rounded up to a whole wave plus one guard wave, so whole-wave reads and the LS
 // receiver's staged groups stay inside the buffer.
 inline int64_t sym_pitch(int64_t n_frames) { return (2 * n_frames + 63) / 64 * 64 + 64; }

@@ -42,6 +42,36 @@ __device__ __forceinline__ void channel_taps(uint32_t f_lo, uint32_t f_hi, uint3
     h[3] = make_float2(s * b.z[2], s * b.z[3]);
 }
 
+// Truth bits in demap order.  The receivers consume the data bins one FFT sub-block at a time: sub-block
+// R holds the bins k = 4 kc + R (kc ascending), 12 / 11 / 14 / 11 data bins for R = 0..3.  Demap word
+// R of a symbol lists, MSB first, for each of those bins the expected sign of the imaginary axis (b0)
+// then of the real axis (b0 ^ b1) -- the non-Gray map of D10: im < 0 iff b0, re < 0 iff b0 != b1 --
+// so the receiver walks it with v_add (t + t, a fast-class shift) instead of per-bin shifts.
+template <int R>
+__host__ __device__ constexpr int demap_bins() {
+    int n = 0;
+    for (int kc = 0; kc < 16; ++kc) n += data_index(4 * kc + R) >= 0;
+    return n;
+}
+template <int R>
+__host__ __device__ inline uint32_t demap_word(const uint32_t w[3]) {
+    uint32_t t = 0u;
+    int pos = 31;
+    for (int kc = 0; kc < 16; ++kc) {
+        const int m = data_index(4 * kc + R);
+        if (m < 0) continue;
+        const uint32_t b0 = (w[(2 * m) >> 5] >> (31 - ((2 * m) & 31))) & 1u;
+        const uint32_t b1 = (w[(2 * m + 1) >> 5] >> (31 - ((2 * m + 1) & 31))) & 1u;
+        t |= b0 << pos;
+        t |= (b0 ^ b1) << (pos - 1);
+        pos -= 2;
+    }
+    return t;
+}
+__host__ __device__ inline void demap_words(const uint32_t w[3], uint32_t t[4]) {
+    t[0] = demap_word<0>(w); t[1] = demap_word<1>(w); t[2] = demap_word<2>(w); t[3] = demap_word<3>(w);
+}
+
 // Per-symbol decisions + metrics, consumed one FFT sub-block at a time.
 //   Z = Y / H (OFDM.c:1044-1052), slicer (OFDM.c:852-871), demap (OFDM.c:873-908), bit compare
 //   (OFDM.c:1154-1161), EVM pre/post (OFDM.c:1104-1150).
@@ -49,10 +79,11 @@ __device__ __forceinline__ void channel_taps(uint32_t f_lo, uint32_t f_hi, uint3
 // The equaliser hands back Z = u * g with g > 0, so the slicer decision is the sign of u:
 //   KIND 0: g = 1 (ideal AWGN), KIND 1: g = r (ideal ZF, r = 1/|H|^2),
 //   KIND 2: g = 2 r (LTF LS: Y / (0.5 Lf S) = 2 Lf Y conj(S) / |S|^2, r = 1/|S|^2).
-// With the truth symbol d = (sr c, si c), c = 1/sqrt2 (non-Gray map, D10: re < 0 iff b0 != b1,
-// im < 0 iff b0), flipping u's sign bits by (sr, si) gives u' with
+// With the truth symbol d = (sr c, si c), c = 1/sqrt2, flipping u's sign bits by the demap word's
+// expected signs gives u' with
 //   |Z - d|^2 = (u'.x g - c)^2 + (u'.y g - c)^2     and     axis error <=> sign bit of u' set,
-// so each bin costs one bitop3 per axis for the truth, one fma per axis for the EVM and one
+// so each bin costs two v_add to advance the demap word, one v_bitop3 per axis for the truth (the
+// sign mask in a VGPR: an SGPR operand issues at the slow rate), one fma per axis for the EVM and one
 // alignbit per axis to collect the errors (popcounted once per sub-block).  Decisions agree with
 // "Z > 0" (OFDM.c:858-866) except for an exactly-zero equalised value.
 template <int KIND>
@@ -72,13 +103,18 @@ __device__ __forceinline__ void sym_init(SymState &st) {
 template <int KIND>
 __device__ __forceinline__ float finish_evm(const SymState &st) { return KIND == 2 ? 4.0f * st.evm_pre : st.evm_pre; }
 
+// t + t as a v_add_u32 (fast class): LLVM would otherwise fold it into a v_lshlrev (slow class)
+__device__ __forceinline__ uint32_t dbl_u32(uint32_t t) {
+    uint32_t r;
+    asm("v_add_u32_e32 %0, %1, %1" : "=v"(r) : "v"(t));
+    return r;
+}
+
+// t: demap word R of this lane's symbol (0 on lanes without a data symbol)
 template <bool DUMP, int R, int KIND, typename HF>
-__device__ __forceinline__ void demap_sub(const float2 (&x)[64], const uint32_t (&wi)[3], HF &&Hof, float2 *dump_eq,
-                                          SymState &st) {
-    uint32_t w[3] = {wi[0], wi[1], wi[2]};
-    opaque(w[0]); opaque(w[1]); opaque(w[2]);     // truth shifts are made here, not hoisted
-    // b0 at bit 31 - 2m of w; b0 ^ b1 at the same position of wx
-    const uint32_t wx[3] = {w[0] ^ (w[0] << 1), w[1] ^ (w[1] << 1), w[2] ^ (w[2] << 1)};
+__device__ __forceinline__ void demap_sub(const float2 (&x)[64], uint32_t t, HF &&Hof, float2 *dump_eq, SymState &st) {
+    uint32_t sm;
+    asm volatile("v_mov_b32 %0, 0x80000000" : "=v"(sm));
     constexpr float cd = KIND == 2 ? 0.5f * INV_SQRT2 : INV_SQRT2;
     uint32_t em = 0u;     // per bin: re error then im error, shifted in from bit 0
     static_for<0, 16>([&](auto kc) {
@@ -86,11 +122,11 @@ __device__ __forceinline__ void demap_sub(const float2 (&x)[64], const uint32_t 
         constexpr int m = data_index(bin);
         if constexpr (m >= 0) {
             const EqOut<KIND> e = Hof(x[digit_rev4(bin)], std::integral_constant<int, bin>{});
-            constexpr int wi = (2 * m) >> 5, sh = (2 * m) & 31;
-            const uint32_t tr = sh ? wx[wi] << sh : wx[wi], ti = sh ? w[wi] << sh : w[wi];
+            const uint32_t ti = t, tr = dbl_u32(t);
+            t = dbl_u32(tr);
             // u' = u ^ (t & 0x80000000): bitop3 table a ^ (b & c) = 0x78
-            const uint32_t ur = __builtin_amdgcn_bitop3_b32(__float_as_uint(e.u.x), tr, 0x80000000u, 0x78);
-            const uint32_t ui = __builtin_amdgcn_bitop3_b32(__float_as_uint(e.u.y), ti, 0x80000000u, 0x78);
+            const uint32_t ur = __builtin_amdgcn_bitop3_b32(__float_as_uint(e.u.x), tr, sm, 0x78);
+            const uint32_t ui = __builtin_amdgcn_bitop3_b32(__float_as_uint(e.u.y), ti, sm, 0x78);
             float ex, ey;
             if constexpr (KIND == 0) {
                 ex = __uint_as_float(ur) - cd;
@@ -107,6 +143,7 @@ __device__ __forceinline__ void demap_sub(const float2 (&x)[64], const uint32_t 
                 const float2 z = KIND == 0 ? e.u : make_float2(e.u.x * g, e.u.y * g);
                 if (dump_eq) dump_eq[m] = z;
                 const uint32_t pr = z.x > 0.f, pi = z.y > 0.f;
+                constexpr int wi = (2 * m) >> 5;
                 constexpr int s0 = 31 - ((2 * m) & 31), s1 = 31 - ((2 * m + 1) & 31);
                 st.d[wi] |= ((pi ^ 1u) << s0) | ((pr ^ pi) << s1);
             }

@@ -149,7 +149,7 @@ __global__ __launch_bounds__(256, 3) void tx_symbols_kernel(TxArgs a) {
     // row-major batch: sample n of symbol sidx at tx[n * pitch + sidx]; the row base
     // is wave-uniform, so each store is saddr + one per-lane offset
     const uint32_t so = (uint32_t)sidx;
-    const int64_t P = a.pitch;
+    [[maybe_unused]] const int64_t P = a.pitch;
     static_for<0, 4>([&](auto rc) {
         constexpr int R = decltype(rc)::value;
         dif_sub16<true, R>(X);
@@ -164,6 +164,11 @@ __global__ __launch_bounds__(256, 3) void tx_symbols_kernel(TxArgs a) {
     a.bits[so] = w[0];
     a.bits[P + so] = w[1];
     a.bits[2 * P + so] = w[2];
+    // rows 3..6: the receivers' demap words (ofdm_rxcommon.h)
+    a.bits[3 * P + so] = demap_word<0>(w);
+    a.bits[4 * P + so] = demap_word<1>(w);
+    a.bits[5 * P + so] = demap_word<2>(w);
+    a.bits[6 * P + so] = demap_word<3>(w);
 }
 
 // ======================================================================== K3: receiver chain
@@ -228,6 +233,31 @@ __device__ __forceinline__ void stage_group(const RxArgs &a, int64_t col0, float
     }
 }
 
+// The group's demap words (Tx rows 3..6, ofdm_rxcommon.h) into LDS by LDS-DMA: wave wv copies row
+// 3 + wv of the n_cols symbols from col0 (4 B per lane, lane l at truth + 4 l).  Columns the DMA does
+// not write stay zero (LS E lanes, the idle lane).
+__device__ __forceinline__ void stage_truth(const RxArgs &a, int64_t col0, uint32_t *truth /* [4][64] */, int wv,
+                                            int lane, int n_cols) {
+    if (lane < n_cols) {
+        const uint32_t *src = a.bits + (3 + wv) * a.pitch + col0 + lane;
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)src,
+                                         (__attribute__((address_space(3))) void *)(truth + 64 * wv), 4, 0, 0);
+    }
+}
+
+// A lane's demap words in LDS, read one sub-block at a time (re-materialised address: the four words
+// are not hoisted out of the SNR loop and held across it)
+typedef __attribute__((address_space(3))) const uint32_t lcu32;
+struct LdsTruth {
+    lcu32 *p;    // &truth[0][column]
+    template <int R>
+    __device__ __forceinline__ uint32_t word() const {
+        lcu32 *q = p;
+        opaque(q);
+        return q[64 * R];
+    }
+};
+
 // Clean samples n0-3..n0+3 (Rayleigh: the 4-tap channel reaches 3 back) or n0..n0+3 of a lane's window.
 template <int CHAN, int N0, typename WS>
 __device__ __forceinline__ void rx_load(float2 (&c)[7], const WS &src) {
@@ -247,19 +277,50 @@ __device__ __forceinline__ void rx_load(float2 (&c)[7], const WS &src) {
 // K = noise_k(sigma) (real) or noise_k(sigma / sqrt2) (complex): each noisy component is one fma.
 // `hd` = philox_head of the frame's noise stream at this SNR point; `tb` = the counter word c2 of
 // the window's first Philox block (t0 / 4 real, t0 / 2 complex).
+// Ablation builds (diagnostics only, results are wrong): OFDM_ABL_NO_PHILOX replaces the Philox
+// rounds by one multiply, OFDM_ABL_NO_BM drops the Box-Muller transcendentals, OFDM_ABL_NO_BPERM
+// equalises with the lane's own bins, OFDM_ABL_NO_DEMAP folds the bins into one sum.  Their run time
+// against the real kernel prices each stage including its stalls.
+// Philox outputs of one group (samples 4g..4g+3 of each quarter): real noise 4 blocks (c2 = tb + g +
+// 4i), complex 8 (c2 = tb + 2g + 8i + {0, 1}), computed together with VGPR round keys.
+template <int NB>
+__device__ __forceinline__ void rx_philox(const PhiloxHead &hd, const uint32_t (&c2)[NB], uint32_t k0, uint32_t k1,
+                                          uint4 (&o)[NB]) {
+#ifdef OFDM_ABL_NO_PHILOX
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const uint64_t p = (uint64_t)PHILOX_M1 * (c2[b] ^ hd.n2);
+        o[b] = make_uint4((uint32_t)p, (uint32_t)(p >> 32), (uint32_t)p ^ hd.c3, (uint32_t)(p >> 32) ^ k0);
+    }
+#elif defined(OFDM_RX_VGPR_KEYS)
+    philox10_c2_vk<NB>(hd, c2, k0, k1, o);      // A/B: c3 -1.9 % (register pressure)
+#else
+#pragma unroll
+    for (int b = 0; b < NB; ++b) o[b] = philox10_c2(hd, c2[b], k0, k1);
+#endif
+}
+__device__ __forceinline__ Noise4 rx_noise4(uint4 o, float K) {
+#ifdef OFDM_ABL_NO_BM
+    Noise4 n;
+    n.r0 = K * (float)o.x; n.r1 = K * (float)o.z;
+    n.c0 = (float)o.y; n.s0 = n.c0 * 0.5f; n.c1 = (float)o.w; n.s1 = n.c1 * 0.5f;
+    return n;
+#else
+    return noise4_of(o, K);
+#endif
+}
+
+// o: the block(s) of samples n0..n0+3 (one for real noise, two for complex)
 template <int NOISE, int CHAN, int N0>
-__device__ __forceinline__ void rx_noisy(float2 (&x)[64], const float2 (&c)[7], const PhiloxHead &hd, uint32_t tb,
-                                         float K, uint32_t k0, uint32_t k1, const float2 (&h)[4]) {
-    // re-materialise per block: keeps LICM from hoisting 16 blocks' worth of round-1 products out
-    // of the SNR loop (tb does not depend on the SNR point)
-    opaque(tb);
+__device__ __forceinline__ void rx_noisy(float2 (&x)[64], const float2 (&c)[7], const uint4 *o, float K,
+                                         const float2 (&h)[4]) {
     float nr[8], nt[8];     // noise of component j = nr[j] * nt[j]
     if constexpr (NOISE == OFDM_NOISE_REAL) {
-        const Noise4 g = noise4_of(philox10_c2(hd, tb + (N0 >> 2), k0, k1), K);
+        const Noise4 g = rx_noise4(o[0], K);
         nr[0] = g.r0; nt[0] = g.c0; nr[1] = g.r0; nt[1] = g.s0; nr[2] = g.r1; nt[2] = g.c1; nr[3] = g.r1; nt[3] = g.s1;
     } else if constexpr (NOISE == OFDM_NOISE_COMPLEX) {
-        const Noise4 g0 = noise4_of(philox10_c2(hd, tb + (N0 >> 1), k0, k1), K);
-        const Noise4 g1 = noise4_of(philox10_c2(hd, tb + (N0 >> 1) + 1, k0, k1), K);
+        const Noise4 g0 = rx_noise4(o[0], K);
+        const Noise4 g1 = rx_noise4(o[1], K);
         nr[0] = g0.r0; nt[0] = g0.c0; nr[1] = g0.r0; nt[1] = g0.s0; nr[2] = g0.r1; nt[2] = g0.c1; nr[3] = g0.r1; nt[3] = g0.s1;
         nr[4] = g1.r0; nt[4] = g1.c0; nr[5] = g1.r0; nt[5] = g1.s0; nr[6] = g1.r1; nt[6] = g1.c1; nr[7] = g1.r1; nt[7] = g1.s1;
     }
@@ -291,6 +352,31 @@ __device__ __forceinline__ void rx_window_stage1(float2 (&x)[64], const WS &src,
     const float K = noise_k(NOISE == OFDM_NOISE_COMPLEX ? sigma * INV_SQRT2 : sigma);
     const PhiloxHead hd = philox_head(f_lo, f_hi, STREAM_NOISE | q, k1);     // shared by the 16-32 blocks
     const uint32_t tb = NOISE == OFDM_NOISE_COMPLEX ? t0 >> 1 : t0 >> 2;
+    constexpr int NB = NOISE == OFDM_NOISE_COMPLEX ? 8 : NOISE == OFDM_NOISE_REAL ? 4 : 1;
+    constexpr int PB = NOISE == OFDM_NOISE_COMPLEX ? 2 : NOISE == OFDM_NOISE_REAL ? 1 : 0;
+    // Philox blocks of group g (samples 4g..4g+3 of each quarter)
+    auto philox_group = [&](auto gc, uint4 (&o)[NB]) {
+        constexpr int g = decltype(gc)::value;
+        if constexpr (NOISE != OFDM_NOISE_NONE) {
+            // re-materialise per group: keeps LICM from hoisting 16 blocks' worth of round-1 products
+            // out of the SNR loop (tb does not depend on the SNR point)
+            uint32_t tg = tb;
+            opaque(tg);
+            uint32_t c2[NB];
+#pragma unroll
+            for (int b = 0; b < NB; ++b)
+                c2[b] = NOISE == OFDM_NOISE_COMPLEX ? tg + 2 * g + 8 * (b >> 1) + (b & 1) : tg + g + 4 * b;
+            rx_philox<NB>(hd, c2, k0, k1, o);
+        }
+    };
+#ifndef OFDM_RX_NO_PIPE_PHILOX
+    // software pipeline: group g + 1's Philox chains share group g's fence region with its Box-Muller,
+    // noise and butterflies (the next group's 16 state VGPRs fit while x is still partly empty).
+    // A/B (profiles/r02/ab): c3 -2.0 %, c2 -4.9 % receiver time
+    uint4 on[NB];
+    philox_group(std::integral_constant<int, 0>{}, on);
+    sched_fence();
+#endif
     static_for<0, 4>([&](auto gc) {
         constexpr int g = decltype(gc)::value;
         float2 c[4][7];
@@ -301,10 +387,18 @@ __device__ __forceinline__ void rx_window_stage1(float2 (&x)[64], const WS &src,
 #ifdef OFDM_RX_EARLY_LOADS
         sched_fence();
 #endif
-        rx_noisy<NOISE, CHAN, 4 * g>(x, c[0], hd, tb, K, k0, k1, h);
-        rx_noisy<NOISE, CHAN, 16 + 4 * g>(x, c[1], hd, tb, K, k0, k1, h);
-        rx_noisy<NOISE, CHAN, 32 + 4 * g>(x, c[2], hd, tb, K, k0, k1, h);
-        rx_noisy<NOISE, CHAN, 48 + 4 * g>(x, c[3], hd, tb, K, k0, k1, h);
+        uint4 o[NB];
+#ifndef OFDM_RX_NO_PIPE_PHILOX
+#pragma unroll
+        for (int b = 0; b < NB; ++b) o[b] = on[b];
+        if constexpr (g < 3) philox_group(std::integral_constant<int, g + 1>{}, on);
+#else
+        philox_group(gc, o);
+#endif
+        rx_noisy<NOISE, CHAN, 4 * g>(x, c[0], o + 0 * PB, K, h);
+        rx_noisy<NOISE, CHAN, 16 + 4 * g>(x, c[1], o + 1 * PB, K, h);
+        rx_noisy<NOISE, CHAN, 32 + 4 * g>(x, c[2], o + 2 * PB, K, h);
+        rx_noisy<NOISE, CHAN, 48 + 4 * g>(x, c[3], o + 3 * PB, K, h);
         static_for<0, 4>([&](auto ic) { dif_stage1<false, 4 * g + decltype(ic)::value>(x); });
         sched_fence();
     });
@@ -313,21 +407,45 @@ __device__ __forceinline__ void rx_window_stage1(float2 (&x)[64], const WS &src,
 // Shared tail: FFT sub-blocks + demap, per-frame combine of the frame's two data symbols
 // (`partner` fetches the other data lane's value), counters.  `leader` lanes (one per valid
 // frame) contribute.
-template <bool DUMP, int KIND, typename HF, typename PF>
-__device__ __forceinline__ void finish_symbol(float2 (&x)[64], const uint32_t (&w)[3], HF &&Hof, PF &&partner,
+template <bool DUMP, int KIND, typename TW, typename HF, typename PF>
+__device__ __forceinline__ void finish_symbol(float2 (&x)[64], const TW &truth, HF &&Hof, PF &&partner,
                                               float2 *dump_eq, uint32_t *dump_bits, bool leader,
                                               unsigned long long *slots, RxStamp &sp) {
     SymState st;
     sym_init(st);
+#ifdef OFDM_RX_PIPE_FFT
+    // software pipeline: sub-block R + 1's FFT (in place, no extra registers) and its equaliser fetch
+    // share sub-block R's demap region.  A/B: c3 +1.2 % receiver time (not adopted)
+    dif_sub16<false, 0>(x);
+    Hof.template prefetch<0>(x);
+    sched_fence();
+    static_for<0, 4>([&](auto rc) {
+        constexpr int R = decltype(rc)::value;
+        demap_sub<DUMP, R, KIND>(x, truth.template word<R>(), Hof, dump_eq, st);
+        if constexpr (R < 3) {
+            dif_sub16<false, R + 1>(x);
+            Hof.template prefetch<R + 1>(x);
+        }
+        sched_fence();
+    });
+#else
     static_for<0, 4>([&](auto rc) {
         constexpr int R = decltype(rc)::value;
         dif_sub16<false, R>(x);
         sp.mark(1);
+#ifdef OFDM_ABL_NO_DEMAP
+        static_for<0, 16>([&](auto kc) {
+            constexpr int bin = 4 * decltype(kc)::value + R;
+            if constexpr (data_index(bin) >= 0) st.evm_pre += x[digit_rev4(bin)].x + x[digit_rev4(bin)].y;
+        });
+#else
         Hof.template prefetch<R>(x);
-        demap_sub<DUMP, R, KIND>(x, w, Hof, dump_eq, st);
+        demap_sub<DUMP, R, KIND>(x, truth.template word<R>(), Hof, dump_eq, st);
+#endif
         sched_fence();
         sp.mark(2);
     });
+#endif
     if constexpr (DUMP) {
         if (dump_bits) { dump_bits[0] = st.d[0]; dump_bits[1] = st.d[1]; dump_bits[2] = st.d[2]; }
     }
@@ -387,6 +505,10 @@ struct LsBpermuteEq {
             constexpr int bin = 4 * decltype(kc)::value + R;
             if constexpr (data_index(bin) >= 0) {
                 const float2 Y = x[digit_rev4(bin)];
+#ifdef OFDM_ABL_NO_BPERM
+                S[decltype(kc)::value] = Y;
+                if (false)
+#endif
                 S[decltype(kc)::value] = make_float2(
                     __int_as_float(__builtin_amdgcn_ds_bpermute((int)e_addr, __float_as_int(Y.x))),
                     __int_as_float(__builtin_amdgcn_ds_bpermute((int)e_addr, __float_as_int(Y.y))));
@@ -417,7 +539,10 @@ __global__ __launch_bounds__(256, OFDM_RX_LS_WAVES) void rx_ls_kernel(RxArgs a) 
     constexpr int NBUF = FADE ? 1 : 2;
     __shared__ unsigned long long sacc[OFDM_MAX_SNR][8];
     __shared__ __attribute__((aligned(16))) float2 sbuf[NBUF][G::BUF_F2];
+    __shared__ uint32_t struth[NBUF][4][64];
     for (int i = threadIdx.x; i < a.n_snr * 8; i += blockDim.x) (&sacc[0][0])[i] = 0ull;
+    for (int i = threadIdx.x; i < NBUF * 4 * 64; i += blockDim.x) (&struth[0][0][0])[i] = 0u;
+    __syncthreads();                                   // zero columns before the first truth DMA
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
     const int fr = lane / 3, role = lane - 3 * fr;     // lane 63: fr 21 (no frame), role 0
@@ -428,11 +553,14 @@ __global__ __launch_bounds__(256, OFDM_RX_LS_WAVES) void rx_ls_kernel(RxArgs a) 
     const uint32_t e_addr = (uint32_t)(3 * fr) << 2;
     const uint32_t d1_addr = (uint32_t)(lane + 1) << 2;
     const int64_t n_groups = (a.n_frames + LS_GROUP_FRAMES - 1) / LS_GROUP_FRAMES;
-    const int64_t P = a.pitch;
+    [[maybe_unused]] const int64_t P = a.pitch;
 
     int cur = 0;
     int64_t grp = blockIdx.x;
-    if (grp < n_groups) stage_group<G>(a, grp * LS_GROUP_SYMS, sbuf[0], a.ltf2_rows, wv, lane);
+    if (grp < n_groups) {
+        stage_group<G>(a, grp * LS_GROUP_SYMS, sbuf[0], a.ltf2_rows, wv, lane);
+        stage_truth(a, grp * LS_GROUP_SYMS, &struth[0][0][0], wv, lane, LS_GROUP_SYMS);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     RxStamp sp;
@@ -442,13 +570,6 @@ __global__ __launch_bounds__(256, OFDM_RX_LS_WAVES) void rx_ls_kernel(RxArgs a) 
         const bool valid = fr < LS_GROUP_FRAMES && fl < a.n_frames;
         const uint64_t f = a.first_frame + (uint64_t)fl;
         const uint32_t f_lo = (uint32_t)f, f_hi = (uint32_t)(f >> 32);
-        uint32_t w[3] = {0u, 0u, 0u};
-        if (!is_e && valid) {
-            const uint32_t so = (uint32_t)(grp * LS_GROUP_SYMS + col);
-            w[0] = a.bits[so]; w[1] = a.bits[P + so]; w[2] = a.bits[2 * P + so];
-        }
-        // land the truth words before the prefetch is queued (vmcnt retires in issue order)
-        opaque(w[0]); opaque(w[1]); opaque(w[2]);
         float2 h[4] = {make_float2(1.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f)};
         const int64_t nxt = grp + gridDim.x;
         if constexpr (FADE) {
@@ -460,17 +581,21 @@ __global__ __launch_bounds__(256, OFDM_RX_LS_WAVES) void rx_ls_kernel(RxArgs a) 
             channel_taps((uint32_t)fg, (uint32_t)(fg >> 32), a.k0, a.k1, hg);
             fade_group<G>(sbuf[0], wv, dcol ? lane : LS_GROUP_SYMS, dcol ? lane : FadeGeom::ECOL + ff, lane < 63, hg);
         } else {
-            if (nxt < n_groups) stage_group<G>(a, nxt * LS_GROUP_SYMS, sbuf[cur ^ 1], a.ltf2_rows, wv, lane);
+            if (nxt < n_groups) {
+                stage_group<G>(a, nxt * LS_GROUP_SYMS, sbuf[cur ^ 1], a.ltf2_rows, wv, lane);
+                stage_truth(a, nxt * LS_GROUP_SYMS, &struth[cur ^ 1][0][0], wv, lane, LS_GROUP_SYMS);
+            }
         }
         LdsRows<G::R0, G::ROW_F2> src;
         src.base = (lcf2 *)(sbuf[FADE ? 0 : cur] + col);
+        LdsTruth truth;
+        truth.p = (lcu32 *)&struth[FADE ? 0 : cur][0][is_e ? LS_GROUP_SYMS : col];
 
         for (int q = wv; q < a.n_snr; q += 4) {
             LdsRows<G::R0, G::ROW_F2> s = src;
-            uint32_t wq[3] = {w[0], w[1], w[2]};
             uint32_t flo = f_lo, fhi = f_hi;
             float2 hq[4] = {h[0], h[1], h[2], h[3]};
-            s.fresh(); opaque(wq[0]); opaque(wq[1]); opaque(wq[2]); opaque(flo); opaque(fhi);
+            s.fresh(); opaque(flo); opaque(fhi);
             const float sg = is_e ? a.sigma[q] * 1.41421356237309504880f : a.sigma[q];
             float2 x[64];
             rx_window_stage1<NOISE, LCHAN>(x, s, flo, fhi, t0, (uint32_t)(a.q_base + q), sg, a.k0, a.k1, hq);
@@ -487,11 +612,14 @@ __global__ __launch_bounds__(256, OFDM_RX_LS_WAVES) void rx_ls_kernel(RxArgs a) 
             LsBpermuteEq Hof;
             Hof.e_addr = e_addr;
             auto partner = [&](uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_bpermute((int)d1_addr, (int)v); };
-            finish_symbol<DUMP, 2>(x, wq, Hof, partner, dump_eq, dump_bits, role == 1 && valid, sacc[q], sp);
+            finish_symbol<DUMP, 2>(x, truth, Hof, partner, dump_eq, dump_bits, role == 1 && valid, sacc[q], sp);
         }
         if constexpr (FADE) {
             __syncthreads();                               // every wave is done with the buffer
-            if (nxt < n_groups) stage_group<G>(a, nxt * LS_GROUP_SYMS, sbuf[0], a.ltf2_rows, wv, lane);
+            if (nxt < n_groups) {
+                stage_group<G>(a, nxt * LS_GROUP_SYMS, sbuf[0], a.ltf2_rows, wv, lane);
+                stage_truth(a, nxt * LS_GROUP_SYMS, &struth[0][0][0], wv, lane, LS_GROUP_SYMS);
+            }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // next group landed
         __syncthreads();                                   // and every wave is done with this one
@@ -512,23 +640,24 @@ __global__ __launch_bounds__(256, OFDM_RX_IDEAL_WAVES) void rx_ideal_kernel(RxAr
     using G = StageGeom<CHAN, 32, 0>;
     __shared__ unsigned long long sacc[OFDM_MAX_SNR][8];
     __shared__ __attribute__((aligned(16))) float2 sbuf[G::BUF_F2];
+    __shared__ uint32_t struth[4][64];
     for (int i = threadIdx.x; i < a.n_snr * 8; i += blockDim.x) (&sacc[0][0])[i] = 0ull;
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
     const int d = lane & 1;
     const uint32_t t0 = 336u + 80u * (uint32_t)d;
     const int64_t n_groups = (2 * a.n_frames + 63) / 64;
-    const int64_t P = a.pitch;
+    [[maybe_unused]] const int64_t P = a.pitch;
     RxStamp sp;
     sp.start();
     for (int64_t grp = blockIdx.x; grp < n_groups; grp += gridDim.x) {
         stage_group<G>(a, grp * 64, sbuf, nullptr, wv, lane);
+        stage_truth(a, grp * 64, &struth[0][0], wv, lane, 64);
         const uint32_t so = (uint32_t)(grp * 64 + lane);
         const int64_t fl = (int64_t)(so >> 1);
         const bool valid = fl < a.n_frames;
         const uint64_t f = a.first_frame + (uint64_t)fl;
         const uint32_t f_lo = (uint32_t)f, f_hi = (uint32_t)(f >> 32);
-        uint32_t w[3] = {a.bits[so], a.bits[P + so], a.bits[2 * P + so]};
         float2 h[4] = {make_float2(1.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f)};
         if constexpr (CHAN == OFDM_CHAN_RAYLEIGH4) channel_taps(f_lo, f_hi, a.k0, a.k1, h);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -536,12 +665,13 @@ __global__ __launch_bounds__(256, OFDM_RX_IDEAL_WAVES) void rx_ideal_kernel(RxAr
         if constexpr (FADE) fade_group<G>(sbuf, wv, lane, lane, true, h);   // column = lane, its frame's taps
         LdsRows<G::R0, G::ROW_F2> src;
         src.base = (lcf2 *)(sbuf + lane);
+        LdsTruth truth;
+        truth.p = (lcu32 *)&struth[0][lane];
         for (int q = wv; q < a.n_snr; q += 4) {
             LdsRows<G::R0, G::ROW_F2> s = src;
-            uint32_t wq[3] = {w[0], w[1], w[2]};
             uint32_t flo = f_lo, fhi = f_hi;
             float2 hq[4] = {h[0], h[1], h[2], h[3]};
-            s.fresh(); opaque(wq[0]); opaque(wq[1]); opaque(wq[2]); opaque(flo); opaque(fhi);
+            s.fresh(); opaque(flo); opaque(fhi);
             if constexpr (CHAN == OFDM_CHAN_RAYLEIGH4) {
                 static_for<0, 4>([&](auto lc) { opaque(hq[decltype(lc)::value].x); opaque(hq[decltype(lc)::value].y); });
             }
@@ -576,7 +706,7 @@ __global__ __launch_bounds__(256, OFDM_RX_IDEAL_WAVES) void rx_ideal_kernel(RxAr
             };
             auto partner = [](uint32_t v) { return dpp_u<DPP_QUAD_XOR1>(v); };
             auto eq = eq_fn(Hof);
-            finish_symbol<DUMP, KIND>(x, wq, eq, partner, dump_eq, dump_bits, d == 0 && valid, sacc[q], sp);
+            finish_symbol<DUMP, KIND>(x, truth, eq, partner, dump_eq, dump_bits, d == 0 && valid, sacc[q], sp);
         }
         __syncthreads();                                   // every wave is done with the group
         sp.mark(4);

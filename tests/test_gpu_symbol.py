@@ -61,11 +61,37 @@ def test_fft64_empty(engine):
 
 
 # ------------------------------------------------------------------ K2
-def tile_symbol(tx, bits, s):
-    """symbol s of the row-major Tx batch (tx[n * pitch + s], bits[k * pitch + s]) -> (80 samples, 3 words)"""
+def tile_symbol(tx, bits, s, demap=False):
+    """symbol s of the row-major Tx batch (tx[n * pitch + s], bits[k * pitch + s]) -> (80 samples, 3 payload
+    words[, 4 demap words])"""
     pitch = tx.numel() // 80
-    return (tx.view(80, pitch)[:, s].cpu().numpy(),
-            bits.view(3, pitch)[:, s].cpu().numpy().astype(np.uint32))
+    rows = bits.view(7, pitch)[:, s].cpu().numpy().astype(np.uint32)
+    out = (tx.view(80, pitch)[:, s].cpu().numpy(), rows[:3])
+    return out + (rows[3:],) if demap else out
+
+
+def data_index(b):
+    """data subcarrier of fftshifted bin b (OFDM.c:528-547), -1 for pilots / nulls / DC"""
+    for lo, hi, off in ((6, 10, 6), (12, 24, 7), (26, 31, 8), (33, 38, 9), (40, 52, 10), (54, 58, 11)):
+        if lo <= b <= hi:
+            return b - off
+    return -1
+
+
+def demap_words(b96):
+    """the receivers' truth words (ofdm_rxcommon.h demap_word): per FFT sub-block R the data bins
+    4 kc + R in order, each as (b0, b0 ^ b1) MSB first"""
+    out = []
+    for R in range(4):
+        t, pos = 0, 31
+        for kc in range(16):
+            m = data_index(4 * kc + R)
+            if m >= 0:
+                b0, b1 = int(b96[2 * m]), int(b96[2 * m + 1])
+                t |= (b0 << pos) | ((b0 ^ b1) << (pos - 1))
+                pos -= 2
+        out.append(t)
+    return np.array(out, np.uint32)
 
 
 @pytest.mark.parametrize("conv", ["c", "matlab"])
@@ -75,12 +101,13 @@ def test_tx_symbols_vs_oracle(engine, oracle, pkg, conv, payload):
     nf = 37  # ragged: not a multiple of a wave (32 frames) or an LS group (21 frames)
     tx, bits = engine.tx_frames(cfg, 1000, nf)
     for s in (0, 1, 17, 2 * nf - 1):
-        samp, words = tile_symbol(tx, bits, s)
+        samp, words, dwords = tile_symbol(tx, bits, s, demap=True)
         gs = 2000 + s
         if payload == "random":
             ref_words = oracle.philox([gs & 0xffffffff, gs >> 32, 0, 0xB1750000], [0x80211A, 0])[:3]
             assert np.array_equal(words, ref_words)
         b = np.array([(int(words[k >> 5]) >> (31 - (k & 31))) & 1 for k in range(96)], np.int32)
+        assert np.array_equal(dwords, demap_words(b))
         if payload == "message":
             assert np.array_equal(b, oracle.message_bits(b"Hey! I am Vivaswan")[96 * (gs & 1):96 * (gs & 1) + 96])
         if payload == "tester":
