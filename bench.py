@@ -284,9 +284,14 @@ def main():
     bytes_per_unit = FRAME_CAPTURE_BYTES / 2 if frame_mode else BYTES_PER_SYMBOL_SNR
     res = pkg.SweepResult(SNR_GRID, c)
     pmc = load_pmc(args.workload)
-    ipu = pmc.get("valu_instr_per_unit")
+    # the receiver kernel this workload launches (ofdm_symbol.hip launch_rx): real-noise AWGN sweeps run
+    # the packed receiver (ofdm_rxpack.hip), the others the {E, D0, D1} LS / ideal receivers
     kernel = ("frame_sync_kernel+frame_sym_kernel" if frame_mode
+              else "rx_pack_kernel" if kw.get("noise") == "real" and kw.get("channel") == "awgn"
               else ("rx_ls_kernel" if kw.get("est") == "ls" else "rx_ideal_kernel"))
+    if pmc and "+".join(pmc.get("kernels", [pmc.get("kernel")])) != kernel:
+        pmc = {}                      # a PMC pass of another kernel: not this run's instruction count
+    ipu = pmc.get("valu_instr_per_unit")
     hbm_alg = units_per_launch * bytes_per_unit / rx_avg_s / 1e9
     tpu = pmc.get("hbm_bytes_per_unit") or (pmc["rx_hbm_bytes_per_launch"] / pmc["units_per_launch"]
                                             if pmc.get("rx_hbm_bytes_per_launch") else None)

@@ -16,7 +16,7 @@ CSRC = PKG_DIR / "csrc"
 INCLUDE = PKG_DIR.parent / "include"
 BUILD = PKG_DIR / "_build"
 LIB = PKG_DIR / "libofdm_mi355x.so"
-SOURCES = ["ofdm_capi.hip", "ofdm_symbol.hip", "ofdm_frame.hip"]
+SOURCES = ["ofdm_capi.hip", "ofdm_symbol.hip", "ofdm_rxpack.hip", "ofdm_frame.hip"]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -fno-slp-vectorize: keep f32 math scalar (packed v_pk_* f32 gives no rate on gfx950 and its
@@ -28,7 +28,8 @@ CFLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-fno-slp-vecto
 
 # per-source flags: the symbol-mode kernels schedule for ILP (A/B: c3 +1 %, c2 +3 %, c5 +3 %; the
 # frame kernels -0.5 %, profiles/r01/ab/ab_*_ilp.json)
-SOURCE_FLAGS = {"ofdm_symbol.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]}
+SOURCE_FLAGS = {"ofdm_symbol.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+                "ofdm_rxpack.hip": []}
 
 
 def _compile(src: str, extra: list[str], build_dir: Path = BUILD) -> Path:

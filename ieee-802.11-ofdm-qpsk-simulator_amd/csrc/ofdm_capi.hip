@@ -282,7 +282,7 @@ int ofdm_tx_bytes(int64_t n_frames, int64_t *tx_bytes, int64_t *bits_bytes) {
         return set_error(OFDM_E_ARG, "n_frames %lld outside [0, %lld]", (long long)n_frames, (long long)MAX_BATCH_FRAMES);
     const int64_t p = sym_pitch(n_frames);
     if (tx_bytes) *tx_bytes = SYM_SAMPLES * p * (int64_t)sizeof(float2);
-    if (bits_bytes) *bits_bytes = 7 * p * (int64_t)sizeof(uint32_t);   // 3 payload words + 4 demap words
+    if (bits_bytes) *bits_bytes = TX_BIT_ROWS * p * (int64_t)sizeof(uint32_t);
     return OFDM_OK;
 }
 

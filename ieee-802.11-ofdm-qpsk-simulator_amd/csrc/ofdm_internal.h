@@ -15,9 +15,11 @@ constexpr int SYM_SAMPLES = 80;        // 64 + 16-sample cyclic prefix (OFDM.c:5
 //   tx  [n * pitch + s] = time sample n (0..79, CP first) of data symbol s = 2 * frame + d
 //   bits[k * pitch + s] = payload word k (MSB-first bits 32k..32k+31) of symbol s, k = 0..2;
 //                         rows k = 3..6: demap word k - 3 (ofdm_rxcommon.h demap_word)
-// pitch = symbols rounded up to a whole wave plus one guard wave, so whole-wave reads and the LS
-// receiver's staged groups stay inside the buffer.
+//                         rows k = 7..9: pair-order word k - 7 (ofdm_rxcommon.h pair_words)
+// pitch = symbols rounded up to a whole wave plus one guard wave, so whole-wave reads and the
+// receivers' groups (LS: 42 symbols, packed: 128 symbols) stay inside the buffer.
 inline int64_t sym_pitch(int64_t n_frames) { return (2 * n_frames + 63) / 64 * 64 + 64; }
+constexpr int TX_BIT_ROWS = 10;
 constexpr int64_t MAX_BATCH_FRAMES = int64_t(1) << 23;   // 80 * pitch fits int32 element offsets
 
 // LS receiver grouping: 21 frames per wave, lanes {E, D0, D1} x 21 + 1 idle
@@ -60,5 +62,9 @@ void launch_fft64(hipStream_t st, const float2 *in, float2 *out, int64_t n, int 
 void launch_tx(hipStream_t st, const TxArgs &a, int conv);
 void launch_rx(hipStream_t st, const RxArgs &a, const ofdm_cfg &cfg, bool dump, unsigned grid);
 int rx_grid(const ofdm_cfg &cfg, int64_t n_frames, int device);
+// K3c (ofdm_rxpack.hip): real-noise AWGN receivers, one frame per lane, two noise windows per FFT
+bool rx_pack_applies(const ofdm_cfg &cfg);
+void launch_rx_pack(hipStream_t st, const RxArgs &a, const ofdm_cfg &cfg, bool dump, unsigned grid);
+int rx_pack_grid(const ofdm_cfg &cfg, int64_t n_frames, int device);
 
 }  // namespace ofdm

@@ -72,6 +72,30 @@ __host__ __device__ inline void demap_words(const uint32_t w[3], uint32_t t[4]) 
     t[0] = demap_word<0>(w); t[1] = demap_word<1>(w); t[2] = demap_word<2>(w); t[3] = demap_word<3>(w);
 }
 
+// Hermitian bin pairs of the packed real-noise receivers (ofdm_rxpack.hip).  The 48 data bins form 24
+// pairs (k, 64 - k), k < 32, listed in the order the receiver consumes them: the pairs of FFT sub-block
+// 0 (k = 0 mod 4), of sub-block 2 (k = 2 mod 4), then the odd k (sub-blocks 1 and 3 together).
+constexpr int PACK_PAIRS = 24;
+__host__ __device__ constexpr int pair_bin(int p) {
+    constexpr int8_t K[PACK_PAIRS] = {8, 12, 16, 20, 24, 28, 6, 10, 14, 18, 22, 26, 30,
+                                      7, 9, 13, 15, 17, 19, 21, 23, 27, 29, 31};
+    return K[p];
+}
+// Pair-order truth words of one symbol (Tx rows 7..9): for each pair p, bins k then 64 - k, each as
+// (b0, b0 ^ b1) MSB first -- 4 bits per pair, 8 pairs per word (the demap_word signs, D10).
+__host__ __device__ inline void pair_words(const uint32_t w[3], uint32_t t[3]) {
+    t[0] = t[1] = t[2] = 0u;
+    for (int p = 0; p < PACK_PAIRS; ++p)
+        for (int h = 0; h < 2; ++h) {
+            const int bin = h ? 64 - pair_bin(p) : pair_bin(p);
+            const int m = data_index(bin);
+            const uint32_t b0 = (w[(2 * m) >> 5] >> (31 - ((2 * m) & 31))) & 1u;
+            const uint32_t b1 = (w[(2 * m + 1) >> 5] >> (31 - ((2 * m + 1) & 31))) & 1u;
+            const int pos = 31 - 4 * (p & 7) - 2 * h;
+            t[p >> 3] |= (b0 << pos) | ((b0 ^ b1) << (pos - 1));
+        }
+}
+
 // Per-symbol decisions + metrics, consumed one FFT sub-block at a time.
 //   Z = Y / H (OFDM.c:1044-1052), slicer (OFDM.c:852-871), demap (OFDM.c:873-908), bit compare
 //   (OFDM.c:1154-1161), EVM pre/post (OFDM.c:1104-1150).
@@ -149,6 +173,9 @@ __device__ __forceinline__ void demap_sub(const float2 (&x)[64], uint32_t t, HF 
             }
         }
     });
+    // pin the sub-block's EVM terms here: left alone, LLVM sinks the fma chain to its single use after
+    // the last sub-block and keeps every bin's u' alive until then (the spills of round 1)
+    opaque(st.evm_pre);
     // im errors at even positions, re errors at odd: b0 wrong <=> im wrong, b1 wrong <=> re ^ im
     st.ax += __popc(em);
     st.be += __popc(em & 0x55555555u) + __popc((em ^ (em >> 1)) & 0x55555555u);

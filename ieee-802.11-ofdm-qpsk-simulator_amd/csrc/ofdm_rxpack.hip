@@ -1,0 +1,371 @@
+// ofdm_rxpack.hip -- K3c: the real-noise symbol-mode receivers (configs c2 / c3, the benchmark).
+//
+// The AWGN the reference adds is real-only (OFDM.c:651, D7) and the receiver's fft() is linear
+// (OFDM.c:314-318), so the spectrum of a received window is the clean symbol's spectrum plus the
+// spectrum of a REAL noise vector:
+//   * the clean spectra depend on the frame, not on the SNR point: a group prologue transforms the
+//     staged Tx samples of 64 frames once (64-point register FFT per symbol) into LDS;
+//   * per SNR point each lane owns ONE frame: its two data windows' noise goes through one complex
+//     64-point FFT as d0 + j d1 (Hermitian split per bin pair (k, 64 - k)), and the LTF pair noise
+//     n1 + n2 through a 32-point FFT of its even/odd samples packed as e[2m] + j e[2m+1];
+//   * the LS estimate S = F1 + F2 = FFT(2T) + FFT(n1 + n2) (OFDM.c:830-850), the ZF equaliser
+//     Z = Y / (0.5 Lf S) (OFDM.c:1044-1052) and the slicer/demap/EVM of both data symbols
+//     (OFDM.c:852-908, 1104-1161) run in the lane that holds S, bin pair by bin pair.
+// Per frame and SNR point that is 1.5 complex FFTs instead of 3, two demaps instead of three
+// (the LTF lane of the {E, D0, D1} layout no longer demaps), no clean-sample loads and no
+// cross-lane traffic.  The noise draws are the same Philox/Box-Muller values as every other receiver
+// (same counters): results agree with the oracle's time-domain chain to fp32 rounding.
+#include "ofdm_internal.h"
+#include "ofdm_rxcommon.h"
+
+#ifndef OFDM_RX_PACK_WAVES
+#define OFDM_RX_PACK_WAVES 2
+#endif
+
+namespace ofdm {
+
+constexpr int PK_FRAMES = 64;              // frames per group: one per lane
+constexpr int PK_SYMS = 2 * PK_FRAMES;     // data symbols per group
+
+// LDS views (address space 3: keeps ds_read after opaque(), which erases provenance)
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const f4v lcf4;
+typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) const u2v lcu2;
+typedef __attribute__((address_space(3))) f2v lf2;
+
+// the LTF noise spectrum E'[k] of the odd-k pairs waits in LDS (per wave) until the odd sub-blocks are
+// consumed: 22 VGPRs less at the register peak (the data FFT's 128 + the even pairs' E')
+#ifndef OFDM_PACK_EE_LDS
+#define OFDM_PACK_EE_LDS 24   // 24 = none: no spill without it (222 VGPRs); A/B option
+#endif
+constexpr int EE_LDS_FIRST = OFDM_PACK_EE_LDS;     // pairs >= this one are parked in LDS
+constexpr int EE_LDS_N = PACK_PAIRS - EE_LDS_FIRST;
+
+// 16-point digit reversal (dif4<16> output order): bin m of a 16-point sub-transform at position rev16(m)
+__host__ __device__ constexpr int rev16(int m) { return ((m & 3) << 2) | (m >> 2); }
+// position of bin k (0..31) of the 32-point transform (radix-2 stage, then two 16-point dif4)
+__host__ __device__ constexpr int pos32(int k) { return (k & 1) ? 16 + rev16(k >> 1) : rev16(k >> 1); }
+
+// Group prologue: clean spectrum of symbol `s` (window rows 16..79 of the Tx batch, times (-1)^n for
+// fft(), OFDM.c:314-318) -> the 24 bin pairs (C[k], C[64 - k]) of spec[p][half][frame].
+__device__ __forceinline__ void clean_spectrum(const RxArgs &a, int64_t s, float4 *spec_col /* &spec[0][half][f] */) {
+    gcf2 *src = (gcf2 *)(a.tx + 16 * a.pitch + s);
+    int P = (int)a.pitch;
+    opaque(P);
+    float2 x[64];
+    static_for<0, 4>([&](auto gc) {
+        constexpr int g = decltype(gc)::value;
+        gcf2 *sp = src;
+        opaque(sp);
+        static_for<0, 16>([&](auto pc) {
+            constexpr int n = 16 * (decltype(pc)::value >> 2) + 4 * g + (decltype(pc)::value & 3);
+            const float2 v = gld(sp, n * P);
+            x[n] = (n & 1) ? make_float2(-v.x, -v.y) : v;
+        });
+        static_for<0, 4>([&](auto ic) { dif_stage1<false, 4 * g + decltype(ic)::value>(x); });
+        sched_fence();
+    });
+    static_for<0, 4>([&](auto rc) { dif_sub16<false, decltype(rc)::value>(x); });
+    static_for<0, PACK_PAIRS>([&](auto pc) {
+        constexpr int p = decltype(pc)::value;
+        constexpr int k = pair_bin(p);
+        const float2 c0 = x[digit_rev4(k)], c1 = x[digit_rev4(64 - k)];
+        spec_col[p * 2 * PK_FRAMES] = make_float4(c0.x, c0.y, c1.x, c1.y);
+    });
+}
+
+// Per-bin demap of one data symbol at one bin: u = Z / g with g > 0 (KIND 0: g = 1, KIND 2: g = 2r),
+// the truth signs walked out of t (2 bits, im then re), EVM and slicer errors (demap_sub's arithmetic,
+// ofdm_rxcommon.h).  DUMP: the equalised value and the decided bits of data subcarrier m.
+template <int KIND, bool DUMP>
+__device__ __forceinline__ void demap_bin(float2 u, float r, uint32_t &t, uint32_t sm, float &evm, uint32_t &em,
+                                          int m, float2 *dump_eq, uint32_t (&dbits)[3]) {
+    constexpr float cd = KIND == 2 ? 0.5f * INV_SQRT2 : INV_SQRT2;
+    const uint32_t ti = t, tr = dbl_u32(t);
+    t = dbl_u32(tr);
+    const uint32_t ur = __builtin_amdgcn_bitop3_b32(__float_as_uint(u.x), tr, sm, 0x78);
+    const uint32_t ui = __builtin_amdgcn_bitop3_b32(__float_as_uint(u.y), ti, sm, 0x78);
+    float ex, ey;
+    if constexpr (KIND == 0) {
+        ex = __uint_as_float(ur) - cd;
+        ey = __uint_as_float(ui) - cd;
+    } else {
+        ex = fmaf(__uint_as_float(ur), r, -cd);
+        ey = fmaf(__uint_as_float(ui), r, -cd);
+    }
+    evm = fmaf(ex, ex, fmaf(ey, ey, evm));
+    em = __builtin_amdgcn_alignbit(em, ur, 31);
+    em = __builtin_amdgcn_alignbit(em, ui, 31);
+    if constexpr (DUMP) {
+        const float g = KIND == 0 ? 1.0f : 2.0f * r;
+        const float2 z = make_float2(u.x * g, u.y * g);
+        if (dump_eq) dump_eq[m] = z;
+        const uint32_t pr = z.x > 0.f, pi = z.y > 0.f;
+        const int wi = (2 * m) >> 5, s0 = 31 - ((2 * m) & 31), s1 = 31 - ((2 * m + 1) & 31);
+        dbits[wi] |= ((pi ^ 1u) << s0) | ((pr ^ pi) << s1);
+    }
+}
+
+// KIND 2: LS estimate from the LTF pair (E spectrum in LDS `ce`, noise from the packed 32-point FFT);
+// KIND 0: ideal channel knowledge (AWGN), Z = Y (times (-1)^bin for the C ifft convention, D5).
+template <int KIND, int CONV, bool DUMP>
+__global__ __launch_bounds__(256, OFDM_RX_PACK_WAVES) void rx_pack_kernel(RxArgs a) {
+    __shared__ __attribute__((aligned(16))) float4 spec[PACK_PAIRS][2][PK_FRAMES];   // 48 KB: (C[k], C[64-k])
+    __shared__ __attribute__((aligned(16))) float4 ce[PACK_PAIRS];                   // LS: FFT((-1)^n 2T[n])
+    __shared__ __attribute__((aligned(8))) uint32_t truth[3][PK_SYMS];               // pair-order words
+    __shared__ unsigned long long sacc[OFDM_MAX_SNR][8];
+    __shared__ __attribute__((aligned(8))) float2 eel[KIND == 2 ? 4 : 1][KIND == 2 && EE_LDS_N > 0 ? EE_LDS_N : 1][KIND == 2 ? 64 : 1];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    for (int i = tid; i < a.n_snr * 8; i += blockDim.x) (&sacc[0][0])[i] = 0ull;
+    if constexpr (KIND == 2) {
+        // the E window's clean samples 2T[n] (both LTF slots hold T): one spectrum per block
+        if (wv == 0) {
+            float2 x[64];
+            static_for<0, 64>([&](auto nc) {
+                constexpr int n = decltype(nc)::value;
+                const float2 v = a.ltf[n];
+                x[n] = (n & 1) ? make_float2(-2.0f * v.x, -2.0f * v.y) : make_float2(2.0f * v.x, 2.0f * v.y);
+            });
+            fft64<false>(x);
+            if (lane == 0) {
+                static_for<0, PACK_PAIRS>([&](auto pc) {
+                    constexpr int p = decltype(pc)::value;
+                    constexpr int k = pair_bin(p);
+                    const float2 c0 = x[digit_rev4(k)], c1 = x[digit_rev4(64 - k)];
+                    ce[p] = make_float4(c0.x, c0.y, c1.x, c1.y);
+                });
+            }
+        }
+    }
+    const int64_t n_groups = (a.n_frames + PK_FRAMES - 1) / PK_FRAMES;
+    for (int64_t grp = blockIdx.x; grp < n_groups; grp += gridDim.x) {
+        __syncthreads();                                   // every wave is done with the last group
+        if (tid < PK_SYMS) {
+            clean_spectrum(a, grp * PK_SYMS + tid, &spec[0][tid & 1][tid >> 1]);
+        } else {
+            const int j = tid - PK_SYMS;
+            const uint32_t *src = a.bits + 7 * a.pitch + grp * PK_SYMS + j;
+            truth[0][j] = src[0];
+            truth[1][j] = src[a.pitch];
+            truth[2][j] = src[2 * a.pitch];
+        }
+        __syncthreads();
+        const int64_t fl = grp * PK_FRAMES + lane;
+        const bool valid = fl < a.n_frames;
+        const uint64_t f = a.first_frame + (uint64_t)fl;
+        for (int q = wv; q < a.n_snr; q += 4) {
+            uint32_t flo = (uint32_t)f, fhi = (uint32_t)(f >> 32);
+            opaque(flo); opaque(fhi);
+            const float sigma = a.sigma[q];
+            const uint32_t qs = STREAM_NOISE | (uint32_t)(a.q_base + q);
+            const PhiloxHead hd = philox_head(flo, fhi, qs, a.k1);
+            // ---- LTF pair noise (LS): e[n] = sqrt2 sigma x Gaussian 192 + n (block 48 + n/4), packed as
+            // z[m] = e'[2m] + j e'[2m+1] with e'[n] = (-1)^n e[n]; radix-2 stage fused, then two dif4<16>
+            float2 z[64];      // z[0..31] used
+            float2 ee[PACK_PAIRS];
+            lf2 *eew = (lf2 *)&eel[KIND == 2 ? wv : 0][0][KIND == 2 ? lane : 0];
+            opaque(eew);
+            if constexpr (KIND == 2) {
+                const float KE = noise_k(sigma * 1.41421356237309504880f);
+                static_for<0, 4>([&](auto ic) {
+                    constexpr int i = decltype(ic)::value;
+                    uint32_t tg = 48u + 2 * i;
+                    opaque(tg);
+                    // blocks b = 2i, 2i+1 (z[4i..4i+3]) and b + 8 (z[4i+16..4i+19])
+                    static_for<0, 2>([&](auto hc) {
+                        constexpr int h = decltype(hc)::value;
+                        const Noise4 lo = noise4_of(philox10_c2(hd, tg + h, a.k0, a.k1), KE);
+                        const Noise4 hi = noise4_of(philox10_c2(hd, tg + 8 + h, a.k0, a.k1), KE);
+                        constexpr int m = 4 * i + 2 * h;
+                        z[m] = make_float2(lo.r0 * lo.c0, -(lo.r0 * lo.s0));
+                        z[m + 1] = make_float2(lo.r1 * lo.c1, -(lo.r1 * lo.s1));
+                        z[m + 16] = make_float2(hi.r0 * hi.c0, -(hi.r0 * hi.s0));
+                        z[m + 17] = make_float2(hi.r1 * hi.c1, -(hi.r1 * hi.s1));
+                    });
+                    static_for<0, 4>([&](auto jc) {
+                        constexpr int j = 4 * i + decltype(jc)::value;
+                        const float2 u = z[j], v = z[j + 16];
+                        z[j] = cadd(u, v);
+                        z[j + 16] = twiddle<2 * j, false>(csub(u, v));     // W32^j
+                    });
+                    sched_fence();
+                });
+                dif4<false, 16, 0>(z);
+                dif4<false, 16, 16>(z);
+                // E'[k] = (Z[k] + conj Z[-k]) / 2 - j W64^k (Z[k] - conj Z[-k]) / 2 (Z indices mod 32), kept
+                // as 2 E'[k] per pair (48 VGPRs instead of the 62 of Z); E'[64 - k] = conj E'[k]
+                static_for<0, PACK_PAIRS>([&](auto pc) {
+                    constexpr int p = decltype(pc)::value;
+                    constexpr int k = pair_bin(p);
+                    const float2 P = z[pos32(k)], Qv = z[pos32(32 - k)];
+                    const float2 F = make_float2(P.x + Qv.x, P.y - Qv.y);
+                    const float2 H = twiddle<k, false>(make_float2(P.x - Qv.x, P.y + Qv.y));
+                    if constexpr (p < EE_LDS_FIRST) {
+                        ee[p] = make_float2(F.x + H.y, F.y - H.x);
+                    } else {
+                        f2v v; v.x = F.x + H.y; v.y = F.y - H.x;
+                        eew[(p - EE_LDS_FIRST) * 64] = v;
+                    }
+                });
+                sched_fence();
+            }
+            // ---- data windows: x[n] = (-1)^n (d0[n] + j d1[n]) fused with the first radix-4 stage.
+            // Gaussian t of the frame's stream is sample t of the frame timeline: D0 at
+            // t = 336 + n (Philox block 84 + n/4), D1 at t = 416 + n (block 104 + n/4).
+            const float K = noise_k(sigma);
+            float2 x[64];
+            static_for<0, 4>([&](auto gc) {
+                constexpr int g = decltype(gc)::value;
+                uint32_t tg = 84u + g;
+                opaque(tg);
+                static_for<0, 4>([&](auto Qc) {
+                    constexpr int Q = decltype(Qc)::value;
+                    const Noise4 n0 = noise4_of(philox10_c2(hd, tg + 4 * Q, a.k0, a.k1), K);
+                    const Noise4 n1 = noise4_of(philox10_c2(hd, tg + 20 + 4 * Q, a.k0, a.k1), K);
+                    const float d0[4] = {n0.r0 * n0.c0, n0.r0 * n0.s0, n0.r1 * n0.c1, n0.r1 * n0.s1};
+                    const float d1[4] = {n1.r0 * n1.c0, n1.r0 * n1.s0, n1.r1 * n1.c1, n1.r1 * n1.s1};
+                    static_for<0, 4>([&](auto ic) {
+                        constexpr int i = decltype(ic)::value;
+                        x[16 * Q + 4 * g + i] = (i & 1) ? make_float2(-d0[i], -d1[i]) : make_float2(d0[i], d1[i]);
+                    });
+#ifndef OFDM_PACK_GEN_SPLIT
+#define OFDM_PACK_GEN_SPLIT 2
+#endif
+                    if constexpr (Q % OFDM_PACK_GEN_SPLIT == OFDM_PACK_GEN_SPLIT - 1 && Q < 3) sched_fence();
+                });
+                static_for<0, 4>([&](auto ic) { dif_stage1<false, 4 * g + decltype(ic)::value>(x); });
+                sched_fence();
+            });
+            // ---- bin pairs: noise split, clean spectra, estimate, equaliser, demap of both data symbols
+            float2 *deq0 = nullptr, *deq1 = nullptr;
+            uint32_t *dbit0 = nullptr, *dbit1 = nullptr;
+            if constexpr (DUMP) {
+                if (valid) {
+                    const int64_t r0 = ((int64_t)q * a.dump_frames + fl) * 2;
+                    deq0 = a.dump_eq + r0 * 48; deq1 = deq0 + 48;
+                    dbit0 = a.dump_bits + r0 * 3; dbit1 = dbit0 + 3;
+                }
+            }
+            uint32_t db0[3] = {0u, 0u, 0u}, db1[3] = {0u, 0u, 0u};
+            lcf4 *sp = (lcf4 *)&spec[0][0][lane];
+            lcu2 *tw = (lcu2 *)&truth[0][2 * lane];
+            opaque(sp); opaque(tw);
+            uint32_t sm;
+            asm volatile("v_mov_b32 %0, 0x80000000" : "=v"(sm));
+            float evm = 0.f;
+            uint32_t em = 0u, be = 0u, ax = 0u, t0 = 0u, t1 = 0u;
+            auto pair = [&](auto pc) {
+                constexpr int p = decltype(pc)::value;
+                constexpr int k = pair_bin(p), k2 = 64 - k;
+                if constexpr ((p & 7) == 0) {
+                    const u2v tt = tw[(p >> 3) * (PK_SYMS / 2)];
+                    t0 = tt.x; t1 = tt.y;
+                }
+                const float2 Zk = x[digit_rev4(k)], Zm = x[digit_rev4(k2)];
+                const float2 A = make_float2(Zk.x + Zm.x, Zk.y - Zm.y), B = make_float2(Zk.x - Zm.x, Zk.y + Zm.y);
+                const f4v c0 = sp[p * 2 * PK_FRAMES], c1 = sp[(p * 2 + 1) * PK_FRAMES];
+                // Y_d = C_d + N_d:  N0[k] = A/2, N0[k'] = conj(A)/2, N1[k] = -j B/2, N1[k'] = conj(N1[k])
+                const float2 y0k = make_float2(fmaf(0.5f, A.x, c0.x), fmaf(0.5f, A.y, c0.y));
+                const float2 y0m = make_float2(fmaf(0.5f, A.x, c0.z), fmaf(-0.5f, A.y, c0.w));
+                const float2 y1k = make_float2(fmaf(0.5f, B.y, c1.x), fmaf(-0.5f, B.x, c1.y));
+                const float2 y1m = make_float2(fmaf(0.5f, B.y, c1.z), fmaf(0.5f, B.x, c1.w));
+                float2 u0k, u0m, u1k, u1m;
+                float rk = 0.f, rm = 0.f;
+                if constexpr (KIND == 2) {
+                    float ex, ey;
+                    if constexpr (p < EE_LDS_FIRST) {
+                        ex = ee[p].x; ey = ee[p].y;
+                    } else {
+                        const f2v v = eew[(p - EE_LDS_FIRST) * 64];
+                        ex = v.x; ey = v.y;
+                    }
+                    const float4 e4 = ce[p];
+                    const float2 Sk = make_float2(fmaf(0.5f, ex, e4.x), fmaf(0.5f, ey, e4.y));
+                    const float2 Sm = make_float2(fmaf(0.5f, ex, e4.z), fmaf(-0.5f, ey, e4.w));
+                    rk = __builtin_amdgcn_rcpf(fmaf(Sk.x, Sk.x, Sk.y * Sk.y));
+                    rm = __builtin_amdgcn_rcpf(fmaf(Sm.x, Sm.x, Sm.y * Sm.y));
+                    // Z = Y / (0.5 Lf S) = 2 Lf Y conj(S) / |S|^2: u = Lf Y conj(S), g = 2 r
+                    u0k = cscale(cmulc(y0k, Sk), (float)ltf_sign(k));
+                    u1k = cscale(cmulc(y1k, Sk), (float)ltf_sign(k));
+                    u0m = cscale(cmulc(y0m, Sm), (float)ltf_sign(k2));
+                    u1m = cscale(cmulc(y1m, Sm), (float)ltf_sign(k2));
+                } else {
+                    constexpr float cs = (CONV == OFDM_CONV_C && (k & 1)) ? -1.0f : 1.0f;   // k, k2 same parity
+                    u0k = cscale(y0k, cs); u0m = cscale(y0m, cs); u1k = cscale(y1k, cs); u1m = cscale(y1m, cs);
+                }
+                demap_bin<KIND, DUMP>(u0k, rk, t0, sm, evm, em, data_index(k), deq0, db0);
+                demap_bin<KIND, DUMP>(u0m, rm, t0, sm, evm, em, data_index(k2), deq0, db0);
+                demap_bin<KIND, DUMP>(u1k, rk, t1, sm, evm, em, data_index(k), deq1, db1);
+                demap_bin<KIND, DUMP>(u1m, rm, t1, sm, evm, em, data_index(k2), deq1, db1);
+                if constexpr ((p & 3) == 3) {
+                    // 16 decisions: im errors at even bit positions, re errors at odd
+                    ax += __popc(em);
+                    be += __popc(em & 0x55555555u) + __popc((em ^ (em >> 1)) & 0x55555555u);
+                    em = 0u;
+                }
+                // pin the per-bin EVM terms here: left alone, LLVM sinks the whole fma chain to its
+                // single use after the last pair and keeps every bin's u' alive until then
+                opaque(evm);
+#ifndef OFDM_PACK_FENCE_PAIRS
+#define OFDM_PACK_FENCE_PAIRS 2
+#endif
+                if constexpr (p % OFDM_PACK_FENCE_PAIRS == OFDM_PACK_FENCE_PAIRS - 1) sched_fence();
+            };
+            dif_sub16<false, 0>(x);
+            static_for<0, 6>(pair);
+            sched_fence();
+            dif_sub16<false, 2>(x);
+            static_for<6, 13>(pair);
+            sched_fence();
+            dif_sub16<false, 1>(x);
+            dif_sub16<false, 3>(x);
+            static_for<13, 24>(pair);
+            if constexpr (DUMP) {
+                if (dbit0) {
+                    dbit0[0] = db0[0]; dbit0[1] = db0[1]; dbit0[2] = db0[2];
+                    dbit1[0] = db1[0]; dbit1[1] = db1[1]; dbit1[2] = db1[2];
+                }
+            }
+            FrameAcc acc;
+            frame_metrics(acc, KIND == 2 ? 4.0f * evm : evm, be, ax);
+            flush_lanes(acc, valid, sacc[q]);
+        }
+    }
+    block_flush(a, sacc);
+}
+
+template <int KIND, int CONV>
+static void launch_pack_t(hipStream_t st, const RxArgs &a, bool dump, unsigned grid) {
+    if (dump) hipLaunchKernelGGL((rx_pack_kernel<KIND, CONV, true>), dim3(grid), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((rx_pack_kernel<KIND, CONV, false>), dim3(grid), dim3(256), 0, st, a);
+}
+
+bool rx_pack_applies(const ofdm_cfg &cfg) {
+#ifdef OFDM_RX_NO_PACK
+    (void)cfg;
+    return false;
+#else
+    return cfg.noise == OFDM_NOISE_REAL && cfg.channel == OFDM_CHAN_AWGN;
+#endif
+}
+
+void launch_rx_pack(hipStream_t st, const RxArgs &a, const ofdm_cfg &cfg, bool dump, unsigned grid) {
+    if (cfg.est == OFDM_EST_LS) launch_pack_t<2, OFDM_CONV_C>(st, a, dump, grid);           // conv via a.ltf
+    else if (cfg.conv == OFDM_CONV_C) launch_pack_t<0, OFDM_CONV_C>(st, a, dump, grid);
+    else launch_pack_t<0, OFDM_CONV_MATLAB>(st, a, dump, grid);
+}
+
+int rx_pack_grid(const ofdm_cfg &cfg, int64_t n_frames, int device) {
+    const int64_t need = (n_frames + PK_FRAMES - 1) / PK_FRAMES;
+    const void *k = cfg.est == OFDM_EST_LS ? reinterpret_cast<const void *>(&rx_pack_kernel<2, OFDM_CONV_C, false>)
+                                           : reinterpret_cast<const void *>(&rx_pack_kernel<0, OFDM_CONV_C, false>);
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1) cus = 256;
+    const int64_t cap = (int64_t)per_cu * cus;
+    const int64_t g = need < cap ? need : cap;
+    return (int)(g < 1 ? 1 : g);
+}
+
+}  // namespace ofdm

@@ -169,6 +169,12 @@ __global__ __launch_bounds__(256, 3) void tx_symbols_kernel(TxArgs a) {
     a.bits[4 * P + so] = demap_word<1>(w);
     a.bits[5 * P + so] = demap_word<2>(w);
     a.bits[6 * P + so] = demap_word<3>(w);
+    // rows 7..9: the packed real-noise receivers' pair-order words (ofdm_rxcommon.h pair_words)
+    uint32_t pw[3];
+    pair_words(w, pw);
+    a.bits[7 * P + so] = pw[0];
+    a.bits[8 * P + so] = pw[1];
+    a.bits[9 * P + so] = pw[2];
 }
 
 // ======================================================================== K3: receiver chain
@@ -752,6 +758,10 @@ static void launch_rx_n(hipStream_t st, const RxArgs &a, int est, int conv, int 
 }
 
 void launch_rx(hipStream_t st, const RxArgs &a, const ofdm_cfg &cfg, bool dump, unsigned grid) {
+    if (rx_pack_applies(cfg)) {
+        launch_rx_pack(st, a, cfg, dump, grid);
+        return;
+    }
     if (dump) {
         switch (cfg.noise) {
             case OFDM_NOISE_REAL: launch_rx_n<OFDM_NOISE_REAL, true>(st, a, cfg.est, cfg.conv, cfg.channel, grid); break;
@@ -768,6 +778,7 @@ void launch_rx(hipStream_t st, const RxArgs &a, const ofdm_cfg &cfg, bool dump, 
 }
 
 int rx_grid(const ofdm_cfg &cfg, int64_t n_frames, int device) {
+    if (rx_pack_applies(cfg)) return rx_pack_grid(cfg, n_frames, device);
     // LS: one block per 21-frame group in flight; ideal: one wave per 64 symbols, 4 waves per block
     // one block per staged group in flight (LS: 21 frames, ideal: 64 symbols)
     const int64_t need = cfg.est == OFDM_EST_LS ? (n_frames + LS_GROUP_FRAMES - 1) / LS_GROUP_FRAMES

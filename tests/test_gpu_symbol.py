@@ -63,11 +63,11 @@ def test_fft64_empty(engine):
 # ------------------------------------------------------------------ K2
 def tile_symbol(tx, bits, s, demap=False):
     """symbol s of the row-major Tx batch (tx[n * pitch + s], bits[k * pitch + s]) -> (80 samples, 3 payload
-    words[, 4 demap words])"""
+    words[, 4 demap words, 3 pair-order words])"""
     pitch = tx.numel() // 80
-    rows = bits.view(7, pitch)[:, s].cpu().numpy().astype(np.uint32)
+    rows = bits.view(10, pitch)[:, s].cpu().numpy().astype(np.uint32)
     out = (tx.view(80, pitch)[:, s].cpu().numpy(), rows[:3])
-    return out + (rows[3:],) if demap else out
+    return out + (rows[3:7], rows[7:]) if demap else out
 
 
 def data_index(b):
@@ -94,6 +94,21 @@ def demap_words(b96):
     return np.array(out, np.uint32)
 
 
+PAIR_BINS = [8, 12, 16, 20, 24, 28, 6, 10, 14, 18, 22, 26, 30, 7, 9, 13, 15, 17, 19, 21, 23, 27, 29, 31]
+
+
+def pair_words(b96):
+    """the packed receivers' truth words (ofdm_rxcommon.h pair_words): per Hermitian pair (k, 64 - k) in
+    consumption order, bins k then 64 - k, each as (b0, b0 ^ b1) MSB first"""
+    bits = []
+    for k in PAIR_BINS:
+        for b in (k, 64 - k):
+            m = data_index(b)
+            b0, b1 = int(b96[2 * m]), int(b96[2 * m + 1])
+            bits += [b0, b0 ^ b1]
+    return np.array([int("".join(map(str, bits[32 * w:32 * w + 32])), 2) for w in range(3)], np.uint32)
+
+
 @pytest.mark.parametrize("conv", ["c", "matlab"])
 @pytest.mark.parametrize("payload", ["random", "message", "tester"])
 def test_tx_symbols_vs_oracle(engine, oracle, pkg, conv, payload):
@@ -101,13 +116,14 @@ def test_tx_symbols_vs_oracle(engine, oracle, pkg, conv, payload):
     nf = 37  # ragged: not a multiple of a wave (32 frames) or an LS group (21 frames)
     tx, bits = engine.tx_frames(cfg, 1000, nf)
     for s in (0, 1, 17, 2 * nf - 1):
-        samp, words, dwords = tile_symbol(tx, bits, s, demap=True)
+        samp, words, dwords, pwords = tile_symbol(tx, bits, s, demap=True)
         gs = 2000 + s
         if payload == "random":
             ref_words = oracle.philox([gs & 0xffffffff, gs >> 32, 0, 0xB1750000], [0x80211A, 0])[:3]
             assert np.array_equal(words, ref_words)
         b = np.array([(int(words[k >> 5]) >> (31 - (k & 31))) & 1 for k in range(96)], np.int32)
         assert np.array_equal(dwords, demap_words(b))
+        assert np.array_equal(pwords, pair_words(b))
         if payload == "message":
             assert np.array_equal(b, oracle.message_bits(b"Hey! I am Vivaswan")[96 * (gs & 1):96 * (gs & 1) + 96])
         if payload == "tester":

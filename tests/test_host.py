@@ -57,7 +57,7 @@ def test_tx_bytes(pkg):
     tb, bb = C.c_int64(), C.c_int64()
     assert lib.ofdm_tx_bytes(17, C.byref(tb), C.byref(bb)) == 0
     # 17 frames = 34 symbols -> pitch = 64 (whole wave) + 64 (guard wave); rows of 80 samples x 8 B
-    assert tb.value == 80 * 128 * 8 and bb.value == 7 * 128 * 4     # 3 payload + 4 demap words
+    assert tb.value == 80 * 128 * 8 and bb.value == 10 * 128 * 4    # 3 payload + 4 demap + 3 pair-order words
     assert lib.ofdm_tx_bytes(1 << 23, C.byref(tb), C.byref(bb)) == 0
     assert lib.ofdm_tx_bytes((1 << 23) + 1, C.byref(tb), C.byref(bb)) == -1     # int32 element offsets
 

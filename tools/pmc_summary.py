@@ -6,7 +6,7 @@ usage: python tools/pmc_summary.py <gpurun_out dir> <workload> <units_total_in_r
 dispatches (warmup steps included), e.g. (warmup + steps) x symbols x 16 SNR points.
 
 Counters are summed over every dispatch of the workload's receiver kernels (symbol mode:
-rx_ls_kernel / rx_ideal_kernel; frame mode: frame_sync_kernel + frame_sym_kernel, which the frame
+rx_pack_kernel (real AWGN) / rx_ls_kernel / rx_ideal_kernel; frame mode: frame_sync_kernel + frame_sym_kernel, which the frame
 timer brackets together) and divided by the units:
   * HBM bytes: FETCH_SIZE (KB) x 1024 x 2 -- gfx950 reports half of the bytes of wide (16 B/lane)
     coalesced streaming reads, LDS-DMA included (MI355X_MICROARCH.md, HBM section) -- plus
@@ -22,8 +22,9 @@ from collections import defaultdict
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-KERNELS = ("rx_ls_kernel", "rx_ideal_kernel", "tx_symbols_kernel", "frame_sync_kernel", "frame_sym_kernel")
-RX_SETS = (("rx_ls_kernel",), ("rx_ideal_kernel",), ("frame_sync_kernel", "frame_sym_kernel"))
+KERNELS = ("rx_pack_kernel", "rx_ls_kernel", "rx_ideal_kernel", "tx_symbols_kernel", "frame_sync_kernel",
+           "frame_sym_kernel")
+RX_SETS = (("rx_pack_kernel",), ("rx_ls_kernel",), ("rx_ideal_kernel",), ("frame_sync_kernel", "frame_sym_kernel"))
 CUS, SIMDS, XCDS = 256, 4, 8
 NOMINAL_CLOCK = 2.4e9
 
