@@ -27,9 +27,10 @@ CFLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-fno-slp-vecto
 
 
 # per-source flags: the symbol-mode kernels schedule for ILP (A/B: c3 +1 %, c2 +3 %, c5 +3 %; the
-# frame kernels -0.5 %, profiles/r01/ab/ab_*_ilp.json)
+# frame kernels -0.5 %, profiles/r01/ab/ab_*_ilp.json; packed receivers c3 +1.4 %, c2 +2.5 %,
+# profiles/r02/ab/SUMMARY.md)
 SOURCE_FLAGS = {"ofdm_symbol.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
-                "ofdm_rxpack.hip": []}
+                "ofdm_rxpack.hip": os.environ.get("OFDM_RXPACK_FLAGS", "-mllvm -amdgpu-sched-strategy=max-ilp").split()}
 
 
 def _compile(src: str, extra: list[str], build_dir: Path = BUILD) -> Path:

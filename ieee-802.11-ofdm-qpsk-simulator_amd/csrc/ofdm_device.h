@@ -91,6 +91,36 @@ __device__ __forceinline__ uint4 philox10_c2(const PhiloxHead &h, uint32_t c2, u
     return make_uint4(c0, c1, c2, c3);
 }
 
+// Round keys k0 + r W0, k1 + r W1 (r = 0..9) held in VGPRs: a v_bitop3_b32 with an SGPR operand issues
+// at the slow rate, with three VGPR operands at the fast rate.  Built once per kernel
+// (asm v_mov: never rematerialised into SGPR form); 20 VGPRs.
+struct PhiloxKeysV {
+    uint32_t k0[10], k1[10];
+    __device__ __forceinline__ void init(uint32_t s0, uint32_t s1) {
+#pragma unroll
+        for (int r = 0; r < 10; ++r) {
+            asm volatile("v_mov_b32 %0, %1" : "=v"(k0[r]) : "s"(s0 + (uint32_t)r * PHILOX_W0));
+            asm volatile("v_mov_b32 %0, %1" : "=v"(k1[r]) : "s"(s1 + (uint32_t)r * PHILOX_W1));
+        }
+    }
+};
+// philox10_c2 with the round keys in VGPRs (same output)
+__device__ __forceinline__ uint4 philox10_c2(const PhiloxHead &h, uint32_t c2, const PhiloxKeysV &k) {
+    const uint64_t p1r = (uint64_t)PHILOX_M1 * c2;
+    uint32_t c0 = __builtin_amdgcn_bitop3_b32((uint32_t)(p1r >> 32), h.c1, k.k0[0], 0x96);
+    uint32_t c1 = (uint32_t)p1r, c3 = h.c3;
+    c2 = h.n2;
+#pragma unroll
+    for (int r = 1; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)PHILOX_M0 * c0;
+        const uint64_t p1 = (uint64_t)PHILOX_M1 * c2;
+        const uint32_t n0 = __builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c1, k.k0[r], 0x96);
+        const uint32_t n2 = __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c3, k.k1[r], 0x96);
+        c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
+    }
+    return make_uint4(c0, c1, c2, c3);
+}
+
 // philox10_c2 for NB blocks at once (same outputs), round keys in VGPRs: a v_bitop3_b32 with an SGPR
 // operand issues at the slow rate, one with three VGPRs at the fast rate.  The keys
 // are moved to VGPRs once and advanced round by round with v_add (literal W0 / W1), shared by the NB

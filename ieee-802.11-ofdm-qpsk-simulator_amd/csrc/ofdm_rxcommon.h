@@ -272,7 +272,8 @@ __device__ __forceinline__ int slot_term(const unsigned long long *s, int k, uns
     }
 }
 
-__device__ __forceinline__ void block_flush(const RxArgs &a, unsigned long long (*sacc)[8]) {
+template <int S>   // slots per SNR point in the block's LDS accumulators (>= 5)
+__device__ __forceinline__ void block_flush(const RxArgs &a, unsigned long long (*sacc)[S]) {
     __syncthreads();
     for (int i = threadIdx.x; i < a.n_snr * 7; i += blockDim.x) {
         const int q = i / 7, k = i % 7;

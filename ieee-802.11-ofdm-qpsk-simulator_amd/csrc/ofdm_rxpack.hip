@@ -18,8 +18,11 @@
 #include "ofdm_internal.h"
 #include "ofdm_rxcommon.h"
 
-#ifndef OFDM_RX_PACK_WAVES
+#ifndef OFDM_RX_PACK_WAVES          // waves per SIMD the LS receiver is register-budgeted for (220 VGPRs)
 #define OFDM_RX_PACK_WAVES 2
+#endif
+#ifndef OFDM_RX_PACK_IDEAL_WAVES    // the ideal-CSI receiver (no LTF spectrum) fits 168 VGPRs / 53 KB LDS
+#define OFDM_RX_PACK_IDEAL_WAVES 3
 #endif
 
 namespace ofdm {
@@ -107,17 +110,43 @@ __device__ __forceinline__ void demap_bin(float2 u, float r, uint32_t &t, uint32
     }
 }
 
+// Ablation builds (diagnostics only, results are wrong; their run time against the real kernel prices a
+// stage including its stalls): OFDM_ABL_NO_PHILOX replaces the Philox rounds by one multiply,
+// OFDM_ABL_NO_BM the Box-Muller transcendentals by multiplies, OFDM_ABL_NO_PREPASS transforms the clean
+// symbols of a block's first group only.
+template <typename KS>
+__device__ __forceinline__ Noise4 pack_noise(const PhiloxHead &hd, uint32_t c2, const KS &keys, uint32_t k1, float K) {
+#ifdef OFDM_ABL_NO_PHILOX
+    (void)keys; (void)k1;
+    const uint64_t p = (uint64_t)PHILOX_M1 * (c2 ^ hd.n2);
+    const uint4 o = make_uint4((uint32_t)p, (uint32_t)(p >> 32), (uint32_t)p ^ hd.c3, (uint32_t)(p >> 32) ^ hd.c1);
+#else
+    uint4 o;
+    if constexpr (std::is_same_v<KS, PhiloxKeysV>) o = philox10_c2(hd, c2, keys);
+    else o = philox10_c2(hd, c2, keys, k1);
+#endif
+#ifdef OFDM_ABL_NO_BM
+    Noise4 n;
+    n.r0 = K * (float)o.x; n.r1 = K * (float)o.z;
+    n.c0 = (float)o.y; n.s0 = n.c0 * 0.5f; n.c1 = (float)o.w; n.s1 = n.c1 * 0.5f;
+    return n;
+#else
+    return noise4_of(o, K);
+#endif
+}
+
 // KIND 2: LS estimate from the LTF pair (E spectrum in LDS `ce`, noise from the packed 32-point FFT);
 // KIND 0: ideal channel knowledge (AWGN), Z = Y (times (-1)^bin for the C ifft convention, D5).
 template <int KIND, int CONV, bool DUMP>
-__global__ __launch_bounds__(256, OFDM_RX_PACK_WAVES) void rx_pack_kernel(RxArgs a) {
+__global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_IDEAL_WAVES) void rx_pack_kernel(RxArgs a) {
     __shared__ __attribute__((aligned(16))) float4 spec[PACK_PAIRS][2][PK_FRAMES];   // 48 KB: (C[k], C[64-k])
     __shared__ __attribute__((aligned(16))) float4 ce[PACK_PAIRS];                   // LS: FFT((-1)^n 2T[n])
     __shared__ __attribute__((aligned(8))) uint32_t truth[3][PK_SYMS];               // pair-order words
-    __shared__ unsigned long long sacc[OFDM_MAX_SNR][8];
+    __shared__ unsigned long long sacc[OFDM_MAX_SNR][5];         // flush_lanes' five slots per SNR point
     __shared__ __attribute__((aligned(8))) float2 eel[KIND == 2 ? 4 : 1][KIND == 2 && EE_LDS_N > 0 ? EE_LDS_N : 1][KIND == 2 ? 64 : 1];
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    for (int i = tid; i < a.n_snr * 8; i += blockDim.x) (&sacc[0][0])[i] = 0ull;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);      // wave-uniform: the SNR loop runs on SGPRs
+    for (int i = tid; i < a.n_snr * 5; i += blockDim.x) (&sacc[0][0])[i] = 0ull;
     if constexpr (KIND == 2) {
         // the E window's clean samples 2T[n] (both LTF slots hold T): one spectrum per block
         if (wv == 0) {
@@ -138,13 +167,29 @@ __global__ __launch_bounds__(256, OFDM_RX_PACK_WAVES) void rx_pack_kernel(RxArgs
             }
         }
     }
+#ifdef OFDM_PACK_VKEYS          // A/B: round keys in VGPRs (fast-class v_bitop3): +0.3 % c3, 20 VGPRs
+    PhiloxKeysV vkeys;
+    vkeys.init(a.k0, a.k1);
+#define PKEYS vkeys, 0u
+#else
+#define PKEYS a.k0, a.k1
+#endif
     const int64_t n_groups = (a.n_frames + PK_FRAMES - 1) / PK_FRAMES;
     for (int64_t grp = blockIdx.x; grp < n_groups; grp += gridDim.x) {
         __syncthreads();                                   // every wave is done with the last group
-        if (tid < PK_SYMS) {
-            clean_spectrum(a, grp * PK_SYMS + tid, &spec[0][tid & 1][tid >> 1]);
+        // group-invariant addresses are re-derived from the thread index here, not held across the SNR
+        // loop (they would be the only values spilled)
+        int t = tid;
+        opaque(t);
+#ifdef OFDM_ABL_NO_PREPASS
+        if (t < PK_SYMS && grp == blockIdx.x) {
+#else
+        if (t < PK_SYMS) {
+#endif
+            clean_spectrum(a, grp * PK_SYMS + t, &spec[0][t & 1][t >> 1]);
+        } else if (t < PK_SYMS) {
         } else {
-            const int j = tid - PK_SYMS;
+            const int j = t - PK_SYMS;
             const uint32_t *src = a.bits + 7 * a.pitch + grp * PK_SYMS + j;
             truth[0][j] = src[0];
             truth[1][j] = src[a.pitch];
@@ -175,8 +220,8 @@ __global__ __launch_bounds__(256, OFDM_RX_PACK_WAVES) void rx_pack_kernel(RxArgs
                     // blocks b = 2i, 2i+1 (z[4i..4i+3]) and b + 8 (z[4i+16..4i+19])
                     static_for<0, 2>([&](auto hc) {
                         constexpr int h = decltype(hc)::value;
-                        const Noise4 lo = noise4_of(philox10_c2(hd, tg + h, a.k0, a.k1), KE);
-                        const Noise4 hi = noise4_of(philox10_c2(hd, tg + 8 + h, a.k0, a.k1), KE);
+                        const Noise4 lo = pack_noise(hd, tg + h, PKEYS, KE);
+                        const Noise4 hi = pack_noise(hd, tg + 8 + h, PKEYS, KE);
                         constexpr int m = 4 * i + 2 * h;
                         z[m] = make_float2(lo.r0 * lo.c0, -(lo.r0 * lo.s0));
                         z[m + 1] = make_float2(lo.r1 * lo.c1, -(lo.r1 * lo.s1));
@@ -221,8 +266,8 @@ __global__ __launch_bounds__(256, OFDM_RX_PACK_WAVES) void rx_pack_kernel(RxArgs
                 opaque(tg);
                 static_for<0, 4>([&](auto Qc) {
                     constexpr int Q = decltype(Qc)::value;
-                    const Noise4 n0 = noise4_of(philox10_c2(hd, tg + 4 * Q, a.k0, a.k1), K);
-                    const Noise4 n1 = noise4_of(philox10_c2(hd, tg + 20 + 4 * Q, a.k0, a.k1), K);
+                    const Noise4 n0 = pack_noise(hd, tg + 4 * Q, PKEYS, K);
+                    const Noise4 n1 = pack_noise(hd, tg + 20 + 4 * Q, PKEYS, K);
                     const float d0[4] = {n0.r0 * n0.c0, n0.r0 * n0.s0, n0.r1 * n0.c1, n0.r1 * n0.s1};
                     const float d1[4] = {n1.r0 * n1.c0, n1.r0 * n1.s0, n1.r1 * n1.c1, n1.r1 * n1.s1};
                     static_for<0, 4>([&](auto ic) {

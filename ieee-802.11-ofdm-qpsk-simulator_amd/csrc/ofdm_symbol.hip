@@ -16,10 +16,10 @@
 #include "ofdm_rxcommon.h"
 
 #ifndef OFDM_RX_LS_WAVES            // waves per SIMD the LS receiver is register-budgeted for
-#define OFDM_RX_LS_WAVES 3
+#define OFDM_RX_LS_WAVES 2      // complex-noise / Rayleigh / noiseless LS: 224 VGPRs, no spill (3: 43-55 spilled, same speed)
 #endif
 #ifndef OFDM_RX_IDEAL_WAVES
-#define OFDM_RX_IDEAL_WAVES 3
+#define OFDM_RX_IDEAL_WAVES 2   // (3: 25-62 spilled)
 #endif
 
 namespace ofdm {
