@@ -546,33 +546,58 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
         // interleaved over the lanes, so a tap's reads are 2 samples apart across lanes (no bank
         // conflicts); clamped reads + select are Convolution's zero padding ----
         bool oob_l = false;
+#ifndef FRAME_MF_U
+#define FRAME_MF_U 1        // matched-filter outputs per lane per pass (A/B: 2 -> -5 %, 4 -> -24 %: registers)
+#endif
+        constexpr int MF_U = FRAME_MF_U;
         // taps copied to VGPRs: an FMA with an SGPR operand issues in the slow class (+0.6 %)
         float tv[21];
 #pragma unroll
         for (int j = 0; j < 21; ++j) asm volatile("v_mov_b32 %0, %1" : "=v"(tv[j]) : "s"(a.taps[j]));
-        for (int ii = tid; ii < nfr; ii += SYNC_THREADS) {
-            const int n = p + 2 * ii;
-            float2 v = make_float2(0.f, 0.f);
-            if (n >= 20 && n < L) {                              // interior: all 21 taps inside
+        // MF_U outputs per lane at once (ii, ii + 128, ...): 2 MF_U independent fma chains instead of 2
+        for (int i0 = tid; i0 < nfr; i0 += MF_U * SYNC_THREADS) {
+            bool inner = true;                                   // every output of the batch interior
 #pragma unroll
-                for (int j = 0; j < 21; ++j) {
-                    const float2 x = r[n - j];
-                    v.x = fmaf(x.x, tv[j], v.x);
-                    v.y = fmaf(x.y, tv[j], v.y);
-                }
-            } else if (n >= L + 20) {
-                oob_l = true;                                    // the reference reads past its buffer
+            for (int u = 0; u < MF_U; ++u) {
+                const int ii = i0 + u * SYNC_THREADS, n = p + 2 * ii;
+                inner = inner && (ii >= nfr || (n >= 20 && n < L));
+            }
+            if (inner) {                                         // all 21 taps inside the capture
+                float2 v[MF_U];
+#pragma unroll
+                for (int u = 0; u < MF_U; ++u) v[u] = make_float2(0.f, 0.f);
+#pragma unroll
+                for (int j = 0; j < 21; ++j)
+#pragma unroll
+                    for (int u = 0; u < MF_U; ++u) {
+                        // outputs past nfr read inside the region (n - j < L) and are not stored
+                        const float2 x = r[min(p + 2 * (i0 + u * SYNC_THREADS), L - 1) - j];
+                        v[u].x = fmaf(x.x, tv[j], v[u].x);
+                        v[u].y = fmaf(x.y, tv[j], v[u].y);
+                    }
+#pragma unroll
+                for (int u = 0; u < MF_U; ++u)
+                    if (i0 + u * SYNC_THREADS < nfr) fr[i0 + u * SYNC_THREADS] = v[u];   // outside every lane's reads
             } else {
+                for (int u = 0; u < MF_U; ++u) {
+                    const int ii = i0 + u * SYNC_THREADS, n = p + 2 * ii;
+                    if (ii >= nfr) break;
+                    float2 v = make_float2(0.f, 0.f);
+                    if (n >= L + 20) {
+                        oob_l = true;                            // the reference reads past its buffer
+                    } else {
 #pragma unroll
-                for (int j = 0; j < 21; ++j) {
-                    const int m = n - j;
-                    float2 x = r[min(max(m, 0), L - 1)];
-                    x = (m >= 0 && m < L) ? x : make_float2(0.f, 0.f);
-                    v.x = fmaf(x.x, tv[j], v.x);
-                    v.y = fmaf(x.y, tv[j], v.y);
+                        for (int j = 0; j < 21; ++j) {
+                            const int m = n - j;
+                            float2 x = r[min(max(m, 0), L - 1)];
+                            x = (m >= 0 && m < L) ? x : make_float2(0.f, 0.f);
+                            v.x = fmaf(x.x, tv[j], v.x);
+                            v.y = fmaf(x.y, tv[j], v.y);
+                        }
+                    }
+                    fr[ii] = v;
                 }
             }
-            fr[ii] = v;                                          // outside every lane's reads
         }
         const bool oob = block_max_i(oob_l ? 1 : 0, redi) != 0;   // also orders fr[] for every lane
         FR_STAMP(3);                                           // matched filter + down-sample
@@ -597,14 +622,23 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
         pp = block_sum_f2(pp, redf);
         double ff = (-1.0 / (2.0 * M_PI * 64.0 * TS)) * (double)atan2f(pp.y, pp.x);
         if (a.float_cfo) ff = (double)(float)ff;
-        // ---- both rotations in one pass (coarse, then fine: OFDM.c:802, 825), the result handed off
-        // directly: LTF1 [192,256), LTF2 [256,320), data d [336 + 80 d, +64) (OFDM.c:830-850,
+        // ---- coarse then fine rotation (OFDM.c:802, 825) as ONE rotation by the summed phase
+        // 2 pi (fc + ff) Ts k, evaluated in fp64 revolutions (the reference's two double-precision
+        // cexp products rounded to float twice; the same rotation to fp32 rounding), the result handed
+        // off directly: LTF1 [192,256), LTF2 [256,320), data d [336 + 80 d, +64) (OFDM.c:830-850,
         // 1024-1040) ----
         const int nw = 2 + a.n_data;
         float2 *dst = a.win + i * (int64_t)(nw * 64);
         const bool dbg = a.dbg_frame && first_item;
+#ifndef OFDM_FRAME_CFO_TWO_STEP
+        const double fcf_ts = (fc + ff) * TS;
+#endif
         for (int k = tid; k < nfr; k += SYNC_THREADS) {
+#ifdef OFDM_FRAME_CFO_TWO_STEP
             const float2 v = cfo_rot(cfo_rot(fr[k], fc * TS, k), ff * TS, k);
+#else
+            const float2 v = cfo_rot(fr[k], fcf_ts, k);
+#endif
             if (dbg) a.dbg_frame[k] = v;
             int w = -1, n = 0;
             if (k >= 192 && k < 320) {

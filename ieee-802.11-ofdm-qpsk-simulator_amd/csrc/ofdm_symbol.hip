@@ -1,16 +1,18 @@
 // ofdm_symbol.hip -- symbol-mode kernels for gfx950 (MI355X): K1 batched FFT, K2 Tx builder,
 // K3 fused AWGN/Rayleigh + receiver chain with counters.  DESIGN.md §2-§4 describe layout,
-// roofline and the RNG spec; the per-stage reference lines are cited inline.
+// roofline and the RNG spec; the per-stage reference lines are cited inline.  The real-noise AWGN
+// sweeps (c2/c3/c4, the benchmark) run the packed receivers of ofdm_rxpack.hip instead (launch_rx);
+// the kernels here serve complex noise, the 4-tap Rayleigh channel (c5) and noiseless runs.
 //
-// Mapping: ONE LANE OWNS ONE 64-SAMPLE WINDOW (a data symbol or one long-training symbol); its
-// 64-point FFT lives in that lane's VGPRs (ofdm_device.h).  In LS mode the four lanes of a DPP
-// quad carry one frame {LTF1, LTF2, D0, D1}: the LS estimate H = 0.5(F1+F2)conj(Lf)
-// (OFDM.c:830-850) is formed with two quad broadcasts, no LDS.
+// Mapping: ONE LANE OWNS ONE 64-SAMPLE WINDOW (a data symbol or the LTF pair); its 64-point FFT
+// lives in that lane's VGPRs (ofdm_device.h).  In LS mode a wave carries 21 frames as lanes
+// {E, D0, D1}: the data lanes fetch S = F1 + F2 (OFDM.c:830-850) from their E lane with ds_bpermute.
 //
 // Register discipline: the first radix-4 stage is fused with sample generation (load + channel +
 // noise) four butterflies at a time, then the four 16-point sub-FFTs run one after another and
-// each sub-block's bins are consumed (demapped or stored) at once.  sched_fence() pins that
-// order so the live set stays ~128 VGPRs + temporaries (3 waves/SIMD, no scratch).
+// each sub-block's bins are consumed (demapped or stored) at once.  sched_fence() pins that order
+// and demap_sub pins its EVM chain, so the live set stays ~128 VGPRs + temporaries: 2 waves/SIMD
+// without scratch (tools/resource_usage.py).
 #include <cstdlib>
 #include "ofdm_internal.h"
 #include "ofdm_rxcommon.h"

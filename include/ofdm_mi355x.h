@@ -120,7 +120,8 @@ int ofdm_fft64(ofdm_ctx *ctx, const void *d_in, void *d_out, int64_t n, int inve
  * first_frame + n_frames) with D = 2 data symbols each (symbol s = 2 * frame + d).  Row-major
  * layout: d_tx[n * pitch + s] = sample n (0..79, CP first) as float2, d_bits[k * pitch
  * + s] = payload word k (MSB-first bits, k = 0..2) as uint32, rows k = 3..6 the receivers' demap words
- * (truth signs in FFT sub-block order), pitch = tx_bytes / (80 * 8).  Buffer sizes:
+ * (truth signs in FFT sub-block order), rows k = 7..9 the packed receivers' truth words (Hermitian bin
+ * pair order), pitch = tx_bytes / (80 * 8).  Buffer sizes:
  * ofdm_tx_bytes(n_frames, &tx_bytes, &bits_bytes); at most 2^23 frames per batch. */
 int ofdm_tx_bytes(int64_t n_frames, int64_t *tx_bytes, int64_t *bits_bytes);
 int ofdm_tx_frames(ofdm_ctx *ctx, const ofdm_cfg *cfg, uint64_t first_frame, int64_t n_frames,
