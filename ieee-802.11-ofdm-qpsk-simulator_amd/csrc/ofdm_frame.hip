@@ -393,15 +393,29 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
 #ifndef FRAME_CAP_U
 #define FRAME_CAP_U 3   // Philox blocks per lane per pass: 752-block captures in 2 full passes (A/B: +1.7 % over 4)
 #endif
+            // The waveform is FR_REPS copies of one filtered frame (OFDM.c:607-612): sample k is sample
+            // k mod nfilt of the first copy, so every trial reads the same 7.8 KB (L1-resident) instead of
+            // its own 24 KB window of the 78 KB waveform.  bm = the block's index within the copy
+            // (nfilt is a multiple of 4; pb > SYNC_THREADS, so one conditional subtract per step).
+            const uint32_t pb = (uint32_t)(a.wave_len / (4 * FR_REPS)), nb_wave = (uint32_t)(a.wave_len / 4);
+            uint32_t bm = (uint32_t)(b0 + tid) % pb;
             for (int bb = b0 + tid; bb <= b1; bb += FRAME_CAP_U * SYNC_THREADS) {
                 float2 v[FRAME_CAP_U][4];
 #pragma unroll
-                for (int u = 0; u < FRAME_CAP_U; ++u)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const int b = bb + SYNC_THREADS * u, k = 4 * b + j;
-                        v[u][j] = (b <= b1 && k < a.wave_len) ? a.wave[k] : make_float2(0.f, 0.f);
-                    }
+                for (int u = 0; u < FRAME_CAP_U; ++u) {
+                    const int b = bb + SYNC_THREADS * u;
+#ifdef OFDM_FRAME_WAVE_FULL     // A/B: read the full 78 KB waveform
+                    const float4 *s4 = reinterpret_cast<const float4 *>(a.wave + 4 * b);
+#else
+                    const float4 *s4 = reinterpret_cast<const float4 *>(a.wave + 4 * bm);
+#endif
+                    const bool in = b <= b1 && (uint32_t)b < nb_wave;
+                    const float4 lo = in ? s4[0] : make_float4(0.f, 0.f, 0.f, 0.f);
+                    const float4 hi = in ? s4[1] : make_float4(0.f, 0.f, 0.f, 0.f);
+                    v[u][0] = make_float2(lo.x, lo.y); v[u][1] = make_float2(lo.z, lo.w);
+                    v[u][2] = make_float2(hi.x, hi.y); v[u][3] = make_float2(hi.z, hi.w);
+                    bm = min(bm + SYNC_THREADS, bm + SYNC_THREADS - pb);     // (bm + 128) mod pb, unsigned
+                }
 #pragma unroll
                 for (int u = 0; u < FRAME_CAP_U; ++u) {
                     const int b = bb + SYNC_THREADS * u;
