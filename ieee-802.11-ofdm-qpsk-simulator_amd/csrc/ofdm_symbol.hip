@@ -13,6 +13,7 @@
 // each sub-block's bins are consumed (demapped or stored) at once.  sched_fence() pins that order
 // and demap_sub pins its EVM chain, so the live set stays ~128 VGPRs + temporaries: 2 waves/SIMD
 // without scratch (tools/resource_usage.py).
+#include <algorithm>
 #include <cstdlib>
 #include "ofdm_internal.h"
 #include "ofdm_rxcommon.h"
@@ -117,6 +118,67 @@ __global__ __launch_bounds__(64, 2) void fft64_kernel(const float2 *__restrict__
             const float2 a = lds[r * K1_ROW + col], b = lds[r * K1_ROW + col + 1];
             dst[e >> 1] = make_float4(a.x, a.y, b.x, b.y);
         }
+    }
+}
+
+// K1 as launched (-DOFDM_K1_LANE selects the kernel above): the north_star's "one FFT per wavefront,
+// radix-4 + __shfl" mapping.  Lane L holds x[L]; each radix-4 DIF stage fetches the four inputs of its
+// butterfly with __shfl (ds_bpermute), forms its own output and applies its twiddle.  K1 is HBM-bound
+// and this mapping streams 3.7-4.2 TB/s against the lane-per-transform kernel's 2.8 TB/s (one wave per
+// SIMD: 174 VGPRs + a 33 KB LDS transpose); it costs ~3.9x the VALU per transform, which is why the
+// VALU-bound receivers keep one window per lane.
+// one radix-4 DIF stage of span 4Q: lane L = base + m Q (+ j) gathers its butterfly's four inputs, forms
+// output m and applies the twiddle w = W_{4Q}^{j m} (precomputed per lane: it does not depend on the
+// transform)
+template <bool INV, int Q>
+__device__ __forceinline__ float2 wave_dif_stage(float2 v, int lane, float2 w) {
+    const int m = (lane / Q) & 3, base = lane - m * Q;
+    float2 a[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int src = base + q * Q;
+        a[q] = make_float2(__shfl(v.x, src, 64), __shfl(v.y, src, 64));
+    }
+    const float2 t0 = cadd(a[0], a[2]), t1 = csub(a[0], a[2]), t2 = cadd(a[1], a[3]), t3 = csub(a[1], a[3]);
+    // y0 = t0 + t2, y2 = t0 - t2, y1 = t1 -/+ j t3, y3 = t1 +/- j t3 (forward / inverse)
+    const float2 jt3 = INV ? make_float2(-t3.y, t3.x) : make_float2(t3.y, -t3.x);
+    const float2 e = (m & 1) ? t1 : t0;
+    const float2 o = (m & 1) ? jt3 : t2;
+    const float2 y = (m == 0 || m == 1) ? cadd(e, o) : csub(e, o);
+    return make_float2(fmaf(y.x, w.x, -y.y * w.y), fmaf(y.x, w.y, y.y * w.x));
+}
+
+template <bool INV, int Q>
+__device__ __forceinline__ float2 wave_twiddle(int lane) {
+    const int m = (lane / Q) & 3, j = lane % Q;
+    float sn, cs;
+    __sincosf((INV ? 6.283185307179586f : -6.283185307179586f) * (float)(j * m) / (float)(4 * Q), &sn, &cs);
+    return make_float2(cs, sn);
+}
+
+#ifndef OFDM_K1_WAVE_T
+#define OFDM_K1_WAVE_T 8    // transforms per wave, their loads issued together (memory-level parallelism)
+#endif
+template <bool INV, int CONV>
+__global__ __launch_bounds__(256) void fft64_wave_kernel(const float2 *__restrict__ in, float2 *__restrict__ out,
+                                                         int64_t n) {
+    constexpr int T = OFDM_K1_WAVE_T;
+    const int lane = threadIdx.x & 63;
+    const int64_t t0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * T;
+    float2 v[T];
+#pragma unroll
+    for (int u = 0; u < T; ++u) v[u] = t0 + u < n ? in[(t0 + u) * 64 + lane] : make_float2(0.f, 0.f);
+    const float2 w16 = wave_twiddle<INV, 16>(lane), w4 = wave_twiddle<INV, 4>(lane);
+    const int k = digit_rev4(lane);                          // lane L ends with bin digit_rev4(L)
+    const float in_sign = ((!INV || CONV == OFDM_CONV_C) && (lane & 1)) ? -1.0f : 1.0f;    // (-1)^n (D5)
+    const float out_scale = INV ? ((k & 1) ? -1.0f / 64.0f : 1.0f / 64.0f) : 1.0f;
+#pragma unroll
+    for (int u = 0; u < T; ++u) {
+        float2 x = cscale(v[u], in_sign);
+        x = wave_dif_stage<INV, 16>(x, lane, w16);
+        x = wave_dif_stage<INV, 4>(x, lane, w4);
+        x = wave_dif_stage<INV, 1>(x, lane, make_float2(1.0f, 0.0f));   // span 4: twiddles are 1
+        if (t0 + u < n) out[(t0 + u) * 64 + k] = cscale(x, out_scale);
     }
 }
 
@@ -726,8 +788,15 @@ __global__ __launch_bounds__(256, OFDM_RX_IDEAL_WAVES) void rx_ideal_kernel(RxAr
 // ======================================================================== launchers
 template <bool INV>
 static void launch_fft_conv(int conv, dim3 g, hipStream_t st, const float2 *in, float2 *out, int64_t n) {
+#ifndef OFDM_K1_LANE
+    const dim3 gw((unsigned)((n + 4 * OFDM_K1_WAVE_T - 1) / (4 * OFDM_K1_WAVE_T)));
+    if (conv == OFDM_CONV_C) hipLaunchKernelGGL((fft64_wave_kernel<INV, OFDM_CONV_C>), gw, dim3(256), 0, st, in, out, n);
+    else hipLaunchKernelGGL((fft64_wave_kernel<INV, OFDM_CONV_MATLAB>), gw, dim3(256), 0, st, in, out, n);
+    (void)g;
+#else
     if (conv == OFDM_CONV_C) hipLaunchKernelGGL((fft64_kernel<INV, OFDM_CONV_C>), g, dim3(64), 0, st, in, out, n);
     else hipLaunchKernelGGL((fft64_kernel<INV, OFDM_CONV_MATLAB>), g, dim3(64), 0, st, in, out, n);
+#endif
 }
 
 void launch_fft64(hipStream_t st, const float2 *in, float2 *out, int64_t n, int inverse, int conv) {
