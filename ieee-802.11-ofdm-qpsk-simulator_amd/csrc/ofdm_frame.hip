@@ -277,7 +277,14 @@ __device__ __forceinline__ float2 cfo_rot(float2 v, double f_ts, int i) {
 
 // ---------------------------------------------------------------- K4b: sync (one block per item)
 // LDS image of one trial (dynamic shared memory, sized per launch by frame_lds_bytes)
-constexpr int SYNC_THREADS = 128;   // two waves share each trial's latency-bound phases
+#ifndef FRAME_SYNC_THREADS
+#define FRAME_SYNC_THREADS 128
+#endif
+constexpr int SYNC_THREADS = FRAME_SYNC_THREADS;   // the waves that share each trial's latency-bound phases
+constexpr int SYNC_WAVES = SYNC_THREADS / 64;
+static_assert(SYNC_WAVES >= 2 && SYNC_WAVES <= 4, "block reductions use 2..4 waves");
+// per-item scratch words after the accumulators: floats [0, 8) (block float sums), ints [8, 32)
+constexpr int RED_WORDS = 32, RED_I_MAX = 0, RED_I_PREFIX = 4, RED_I_MINMAX = 8;
 constexpr int ACC_SLOTS = 12;       // per-SNR block accumulators: 9 counter sums + word-length min / max
 __host__ __device__ inline int cross_words(int cap_len) { return (cap_len - 47 + 63) / 64 + 1; }
 // capture region: cap_len + 8 samples, the capture starting at sample (rx_start & 3) so that every
@@ -296,49 +303,64 @@ __host__ __device__ inline size_t frame_lds_bytes(int cap_len, int n_data, int n
 #else
     const bool in_cap = fr_in_capture(cap_len, n_data);
 #endif
-    return (size_t)cap_region(cap_len) * 8 + (size_t)cross_words(cap_len) * 8 + (size_t)n_snr * ACC_SLOTS * 8 + 64 +
-           (in_cap ? 0 : (size_t)fr_len(n_data) * 8);
+    return (size_t)cap_region(cap_len) * 8 + (size_t)cross_words(cap_len) * 8 + (size_t)n_snr * ACC_SLOTS * 8 +
+           RED_WORDS * 4 + (in_cap ? 0 : (size_t)fr_len(n_data) * 8);
 }
 
-// block-wide reductions over the two waves (scratch: 2 slots in `red`)
+// block-wide reductions over the SYNC_WAVES waves, the wave partials combined in wave order
 __device__ __forceinline__ float block_sum_f(float v, float *red) {
     v = wave_sum_f(v);
     __syncthreads();
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
     __syncthreads();
-    return red[0] + red[1];
+    float t = red[0];
+#pragma unroll
+    for (int w = 1; w < SYNC_WAVES; ++w) t += red[w];
+    return t;
 }
-// the sum of a float pair over the two waves (scratch: 4 slots), in the same order as block_sum_f
+// the sum of a float pair (scratch: 2 SYNC_WAVES slots), in the same order as block_sum_f
 __device__ __forceinline__ float2 block_sum_f2(float2 v, float *red) {
     v.x = wave_sum_f(v.x);
     v.y = wave_sum_f(v.y);
     __syncthreads();
     if ((threadIdx.x & 63) == 0) { red[2 * (threadIdx.x >> 6)] = v.x; red[2 * (threadIdx.x >> 6) + 1] = v.y; }
     __syncthreads();
-    return make_float2(red[0] + red[2], red[1] + red[3]);
+    float2 t = make_float2(red[0], red[1]);
+#pragma unroll
+    for (int w = 1; w < SYNC_WAVES; ++w) { t.x += red[2 * w]; t.y += red[2 * w + 1]; }
+    return t;
 }
 __device__ __forceinline__ int block_max_i(int v, int *red) {
     v = wave_max_i(v);
     __syncthreads();
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
     __syncthreads();
-    return max(red[0], red[1]);
+    int t = red[0];
+#pragma unroll
+    for (int w = 1; w < SYNC_WAVES; ++w) t = max(t, red[w]);
+    return t;
 }
-// (min of a, max of b) over the two waves in one exchange (scratch: 4 slots)
+// (min of a, max of b) over the waves in one exchange (scratch: 2 SYNC_WAVES slots)
 __device__ __forceinline__ int2 block_minmax_i(int a, int b, int *red) {
     a = wave_min_i(a);
     b = wave_max_i(b);
     __syncthreads();
     if ((threadIdx.x & 63) == 0) { red[2 * (threadIdx.x >> 6)] = a; red[2 * (threadIdx.x >> 6) + 1] = b; }
     __syncthreads();
-    return make_int2(min(red[0], red[2]), max(red[1], red[3]));
+    int2 t = make_int2(red[0], red[1]);
+#pragma unroll
+    for (int w = 1; w < SYNC_WAVES; ++w) { t.x = min(t.x, red[2 * w]); t.y = max(t.y, red[2 * w + 1]); }
+    return t;
 }
 __device__ __forceinline__ int block_min_i(int v, int *red) {
     v = wave_min_i(v);
     __syncthreads();
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
     __syncthreads();
-    return min(red[0], red[1]);
+    int t = red[0];
+#pragma unroll
+    for (int w = 1; w < SYNC_WAVES; ++w) t = min(t, red[w]);
+    return t;
 }
 
 #ifndef FRAME_SYNC_MINB
@@ -353,8 +375,8 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
     unsigned long long *cross = reinterpret_cast<unsigned long long *>(rbase + cap_region(L));
     unsigned long long *acc = cross + cross_words(L);
     float *redf = reinterpret_cast<float *>(acc + a.n_snr * ACC_SLOTS);
-    int *redi = reinterpret_cast<int *>(redf + 4);
-    float2 *const fr_sep = reinterpret_cast<float2 *>(redf + 16);   // used when !fr_in_capture
+    int *redi = reinterpret_cast<int *>(redf + 8);
+    float2 *const fr_sep = reinterpret_cast<float2 *>(redf + RED_WORDS);   // used when !fr_in_capture
     float2 *fr = fr_sep;
     for (int i = tid; i < a.n_snr * ACC_SLOTS; i += SYNC_THREADS) {
         const int k = i % ACC_SLOTS;
@@ -368,6 +390,13 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
     unsigned long long stamp_t = __builtin_amdgcn_s_memtime();
 #endif
     for (int64_t i = blockIdx.x; i < a.n_items; i += gridDim.x) {
+#ifndef FRAME_HOIST_LANE
+        // lane-derived values (addresses, sample indices, fp64 instants) are re-derived per item instead of
+        // being hoisted out of the item loop and held in ~40 VGPRs across every phase
+        int tid = threadIdx.x;
+        opaque(tid);
+        const int lane = tid & 63;
+#endif
         const int64_t g = a.item0 + i;
         const int q = (int)(g % a.n_snr);
         const int64_t ti = g / a.n_snr;
@@ -462,7 +491,8 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
             if (lane == 0) { redf[2 * (tid >> 6)] = mn; redf[2 * (tid >> 6) + 1] = mx; }
             __syncthreads();
             if (tid == 0) {
-                const float bmn = fminf(redf[0], redf[2]), bmx = fmaxf(redf[1], redf[3]);
+                float bmn = redf[0], bmx = redf[1];
+                for (int w = 1; w < SYNC_WAVES; ++w) { bmn = fminf(bmn, redf[2 * w]); bmx = fmaxf(bmx, redf[2 * w + 1]); }
                 unsigned long long *sl = acc + q * ACC_SLOTS;
                 sl[10] = (unsigned long long)min((long long)sl[10], (long long)__float2ll_rn(bmn * (float)OFDM_EVM_Q_SCALE));
                 sl[11] = (unsigned long long)max((long long)sl[11], (long long)__float2ll_rn(bmx * (float)OFDM_EVM_Q_SCALE));
@@ -486,7 +516,10 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
             }
             // batches of DET_B positions (the 2961-position capture gives chunks of 25 = 5 x 5); the
             // batch's crossings are collected with constant shifts and placed once per batch
-            constexpr int DET_B = 5;
+#ifndef FRAME_DET_B
+#define FRAME_DET_B 5
+#endif
+            constexpr int DET_B = FRAME_DET_B;
             for (int nb = n0; nb < n1; nb += DET_B) {
                 float2 o0[DET_B], o1[DET_B], i0[DET_B], i1[DET_B];
 #pragma unroll
@@ -538,14 +571,14 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
         }
         int prev = __shfl_up(pm, 1, 64);
         if (lane == 0) prev = -1;
-        if (lane == 63) redi[2 + (tid >> 6)] = pm;  // wave 0's last crossing -> wave 1's prefix
+        if (lane == 63) redi[RED_I_PREFIX + (tid >> 6)] = pm;   // each wave's last crossing
         __syncthreads();                            // crossing words and wave prefixes are in LDS
-        if (tid >= 64) prev = max(prev, redi[2]);
+        for (int w = 0; w < (tid >> 6); ++w) prev = max(prev, redi[RED_I_PREFIX + w]);   // earlier waves
         const int front = (first >= 0 && first - prev > 300) ? first : -1;
         FR_STAMP(1);                                           // packet detection
         const bool valid = front >= 0 && front + 230 < Lc && bit_at(cross, front + 230);
         // the first valid front that has a later front: the least valid front, unless it is the last one
-        const int2 mm = block_minmax_i(valid ? front : 0x7fffffff, front, redi + 4);
+        const int2 mm = block_minmax_i(valid ? front : 0x7fffffff, front, redi + RED_I_MINMAX);
         const int cand = mm.x < mm.y ? mm.x : 0x7fffffff;
         const bool sync_fail = cand == 0x7fffffff;
         const int p = sync_fail ? 0 : cand + 10 + 1;           // len_RRC_rx + 1 (OFDM.c:758)
@@ -566,8 +599,13 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
         constexpr int MF_U = FRAME_MF_U;
         // taps copied to VGPRs: an FMA with an SGPR operand issues in the slow class (+0.6 %)
         float tv[21];
+#ifdef FRAME_TAPS_SGPR
+#pragma unroll
+        for (int j = 0; j < 21; ++j) tv[j] = a.taps[j];
+#else
 #pragma unroll
         for (int j = 0; j < 21; ++j) asm volatile("v_mov_b32 %0, %1" : "=v"(tv[j]) : "s"(a.taps[j]));
+#endif
         // MF_U outputs per lane at once (ii, ii + 128, ...): 2 MF_U independent fma chains instead of 2
         for (int i0 = tid; i0 < nfr; i0 += MF_U * SYNC_THREADS) {
             bool inner = true;                                   // every output of the batch interior

@@ -143,6 +143,7 @@ __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_
     __shared__ __attribute__((aligned(16))) float4 ce[PACK_PAIRS];                   // LS: FFT((-1)^n 2T[n])
     __shared__ __attribute__((aligned(8))) uint32_t truth[3][PK_SYMS];               // pair-order words
     __shared__ unsigned long long sacc[OFDM_MAX_SNR][5];         // flush_lanes' five slots per SNR point
+    __shared__ uint32_t pf_dummy[64];                             // L2 warm-up destination (never read)
     __shared__ __attribute__((aligned(8))) float2 eel[KIND == 2 ? 4 : 1][KIND == 2 && EE_LDS_N > 0 ? EE_LDS_N : 1][KIND == 2 ? 64 : 1];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);      // wave-uniform: the SNR loop runs on SGPRs
@@ -194,6 +195,20 @@ __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_
             truth[0][j] = src[0];
             truth[1][j] = src[a.pitch];
             truth[2][j] = src[2 * a.pitch];
+#ifndef OFDM_PACK_NO_L2_WARM
+            // warm L2 with this block's next group (64 rows x 1 KB: one 4-byte LDS-DMA read per 128-B line,
+            // into a dummy LDS word), so the next prologue's loads hit L2 instead of HBM
+            const int64_t ng = grp + gridDim.x;
+            if (ng < n_groups) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int line = j + PK_SYMS * i;                       // 0..511
+                    const float2 *p = a.tx + (int64_t)(16 + (line >> 3)) * a.pitch + ng * PK_SYMS + (line & 7) * 16;
+                    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)p,
+                                                     (__attribute__((address_space(3))) void *)pf_dummy, 4, 0, 0);
+                }
+            }
+#endif
         }
         __syncthreads();
         const int64_t fl = grp * PK_FRAMES + lane;
