@@ -5,7 +5,9 @@ next to this file, so the .so travels to the GPU box with the repository snapsho
 """
 from __future__ import annotations
 
+import json
 import os
+import re
 import subprocess
 import sys
 from concurrent.futures import ThreadPoolExecutor
@@ -33,13 +35,52 @@ SOURCE_FLAGS = {"ofdm_symbol.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
                 "ofdm_rxpack.hip": os.environ.get("OFDM_RXPACK_FLAGS", "-mllvm -amdgpu-sched-strategy=max-ilp").split()}
 
 
-def _compile(src: str, extra: list[str], build_dir: Path = BUILD) -> Path:
+# Kernels whose parity-dump variants (last template argument `true`) are allowed to spill: they
+# write every equalised bin and run only in tests.  Every other kernel must build spill-free.
+DUMP_KERNEL = re.compile(r"^ofdm::(rx_\w+|frame_sym)_kernel<.*true>$")
+RESOURCE_REPORT = BUILD / "resource_usage.json"
+
+
+def parse_resource_usage(stderr: str) -> list[dict]:
+    """Per-kernel rows of hipcc's -Rpass-analysis=kernel-resource-usage remarks (demangled names)."""
+    rows, cur = [], None
+    for line in stderr.splitlines():
+        m = re.search(r"remark: +(Function Name|VGPRs|AGPRs|VGPRs Spill|SGPRs|SGPRs Spill|ScratchSize \[bytes/lane\]|"
+                      r"LDS Size \[bytes/block\]|Occupancy \[waves/SIMD\]): (\S+)", line)
+        if not m:
+            continue
+        k, v = m.groups()
+        if k == "Function Name":
+            cur = {"mangled": v}
+            rows.append(cur)
+        elif cur is not None:
+            cur[k] = int(v) if v.lstrip("-").isdigit() else v
+    dem = subprocess.run(["c++filt"], input="\n".join(x["mangled"] for x in rows), capture_output=True, text=True)
+    names = dem.stdout.splitlines() if dem.returncode == 0 and rows else [x["mangled"] for x in rows]
+    for x, n in zip(rows, names):
+        x["name"] = re.sub(r"\(.*", "", n).replace("void ", "")
+        x["dump_variant"] = bool(DUMP_KERNEL.match(x["name"]))
+    return rows
+
+
+def spilling_kernels(rows: list[dict]) -> list[str]:
+    """Non-dump kernels with a VGPR spill or scratch use (SGPR spills land in VGPR lanes, not scratch)."""
+    return [f"{x['name']}: {x.get('VGPRs Spill')} VGPR spilled, {x.get('ScratchSize [bytes/lane]')} B scratch/lane"
+            for x in rows if not x["dump_variant"]
+            and (x.get("VGPRs Spill", 0) or x.get("ScratchSize [bytes/lane]", 0))]
+
+
+def _compile(src: str, extra: list[str], build_dir: Path = BUILD) -> tuple[Path, list[dict]]:
     obj = build_dir / (Path(src).stem + ".o")
-    cmd = [HIPCC, *CFLAGS, *SOURCE_FLAGS.get(src, []), *extra, "-c", str(CSRC / src), "-o", str(obj)]
+    cmd = [HIPCC, *CFLAGS, *SOURCE_FLAGS.get(src, []), *extra, "-c", str(CSRC / src), "-o", str(obj),
+           "-Rpass-analysis=kernel-resource-usage"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-6000:]}")
-    return obj
+    rows = parse_resource_usage(r.stderr)
+    for x in rows:
+        x["source"] = src
+    return obj, rows
 
 
 def _stale() -> bool:
@@ -60,7 +101,14 @@ def build(force: bool = False, extra: list[str] | None = None, verbose: bool = T
     build_dir.mkdir(parents=True, exist_ok=True)
     extra = extra or []
     with ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
-        objs = list(ex.map(lambda s: _compile(s, extra, build_dir), SOURCES))
+        done = list(ex.map(lambda s: _compile(s, extra, build_dir), SOURCES))
+    objs = [o for o, _ in done]
+    rows = [x for _, r in done for x in r]
+    (build_dir / RESOURCE_REPORT.name).write_text(json.dumps(rows, indent=1))
+    if out is None:
+        bad = spilling_kernels(rows)
+        if bad:
+            raise RuntimeError("kernels on the product path spill to scratch:\n  " + "\n  ".join(bad))
     tmp = lib.with_suffix(".so.tmp")
     cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp)]
     r = subprocess.run(cmd, capture_output=True, text=True)

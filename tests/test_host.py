@@ -36,6 +36,20 @@ def test_library_has_gfx950_code_object(pkg):
     assert b"amdgcn-amd-amdhsa--gfx950" in blob
 
 
+def test_product_kernels_do_not_spill(pkg):
+    # build_lib writes hipcc's resource-usage remarks next to the objects and refuses a spilling build;
+    # this re-reads that report so a stale library built before the check cannot slip through
+    from ofdm_amd import build_lib
+    if not build_lib.RESOURCE_REPORT.exists():
+        pytest.skip("library not built in this tree (no resource report)")
+    rows = json.loads(build_lib.RESOURCE_REPORT.read_text())
+    names = {x["name"] for x in rows}
+    for k in ("ofdm::rx_pack_kernel<0, 0, false>", "ofdm::frame_sync_kernel", "ofdm::frame_sym_kernel<false>",
+              "ofdm::rx_ls_kernel<1, 1, false>", "ofdm::tx_symbols_kernel<0>"):
+        assert k in names, k
+    assert build_lib.spilling_kernels(rows) == []
+
+
 def test_struct_layout(pkg):
     import ctypes as C
     assert C.sizeof(pkg.abi.Cfg) == 48
