@@ -177,13 +177,15 @@ __global__ __launch_bounds__(256) void ota_kernel(const float2 *x, float2 *y, in
     const int b = blockIdx.x * blockDim.x + threadIdx.x;     // one Philox block = 4 samples
     if (4 * b >= n) return;
     const float sigma = (float)sqrt(*power / snr_lin);
-    const Gauss4 g = gauss4(t_lo, t_hi, (uint32_t)b, STREAM_NOISE | q, k0, k1);
+    // the same fp32 arithmetic as frame_sync_kernel's capture, so one stream gives one capture
+    const Noise4 nz = noise4_of(philox10(t_lo, t_hi, (uint32_t)b, STREAM_NOISE | q, k0, k1), noise_k(sigma));
+    const float zr[4] = {nz.r0, nz.r0, nz.r1, nz.r1}, zc[4] = {nz.c0, nz.s0, nz.c1, nz.s1};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int k = 4 * b + j;
         if (k < n) {
             float2 v = x[k];
-            v.x = fmaf(sigma, g.z[j], v.x);
+            v.x = fmaf(zr[j], zc[j], v.x);
             y[k] = v;
         }
     }
@@ -273,6 +275,15 @@ __device__ __forceinline__ float2 cfo_rot(float2 v, double f_ts, int i) {
     s = __builtin_amdgcn_sinf(fr);
     c = __builtin_amdgcn_cosf(fr);
     return make_float2(v.x * c - v.y * s, v.x * s + v.y * c);
+}
+
+// j-th frame sample the receiver reads (j < 160 + 64 nd): the coarse-CFO lag window [80, 112)
+// (OFDM.c:786-792), LTF1 + LTF2 [192, 320) (809-815, 830-850), data symbol d's FFT window [336 + 80 d, +64)
+__device__ __forceinline__ int needed_k(int j) {
+    if (j < 32) return 80 + j;
+    if (j < 160) return 160 + j;
+    const int e = j - 160;
+    return 336 + 80 * (e >> 6) + (e & 63);
 }
 
 // ---------------------------------------------------------------- K4b: sync (one block per item)
@@ -398,8 +409,16 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
         const int lane = tid & 63;
 #endif
         const int64_t g = a.item0 + i;
-        const int q = (int)(g % a.n_snr);
-        const int64_t ti = g / a.n_snr;
+        int q;
+        int64_t ti;
+        if ((uint64_t)g >> 32 == 0) {        // 32-bit division while it fits (~120 SALU less per item)
+            const uint32_t g32 = (uint32_t)g, d = (uint32_t)a.n_snr;
+            ti = g32 / d;
+            q = (int)(g32 - (uint32_t)ti * d);
+        } else {
+            q = (int)(g % a.n_snr);
+            ti = g / a.n_snr;
+        }
         const uint64_t t = a.first_trial + (uint64_t)ti;
         const uint32_t t_lo = (uint32_t)t, t_hi = (uint32_t)(t >> 32), qs = (uint32_t)(a.q_base + q);
         const float sigma = a.sigma[q];
@@ -416,6 +435,7 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
         } else {
             const int b0 = rx_start >> 2, b1 = (rx_start + L - 1) >> 2;
             const PhiloxHead hd = philox_head(t_lo, t_hi, STREAM_NOISE | qs, a.k1);   // shared by all blocks
+            const float Ksig = noise_k(sigma);
             // Gaussian k of the trial's stream goes to waveform sample k (as if Transmission_Over_Air
             // had drawn the whole waveform); only the captured samples are ever evaluated.
             // FRAME_CAP_U Philox blocks per lane per pass, their waveform loads issued first.
@@ -445,17 +465,30 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
                     v[u][2] = make_float2(hi.x, hi.y); v[u][3] = make_float2(hi.z, hi.w);
                     bm = min(bm + SYNC_THREADS, bm + SYNC_THREADS - pb);     // (bm + 128) mod pb, unsigned
                 }
+#ifdef OFDM_FRAME_CAP_VKEYS   // A/B: the pass's Philox blocks together, round keys in VGPRs
+                uint4 po[FRAME_CAP_U];
+                if (a.noise == OFDM_NOISE_REAL) {
+                    uint32_t c2s[FRAME_CAP_U];
+#pragma unroll
+                    for (int u = 0; u < FRAME_CAP_U; ++u) c2s[u] = (uint32_t)(bb + SYNC_THREADS * u);
+                    philox10_c2_vk<FRAME_CAP_U>(hd, c2s, a.k0, a.k1, po);
+                }
+#endif
 #pragma unroll
                 for (int u = 0; u < FRAME_CAP_U; ++u) {
                     const int b = bb + SYNC_THREADS * u;
                     if (b > b1) break;
-                    Gauss4 gz;
-                    if (a.noise == OFDM_NOISE_REAL) gz = gauss4_of(philox10_c2(hd, (uint32_t)b, a.k0, a.k1));
                     float2 w[4];
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        w[j] = v[u][j];
-                        if (a.noise == OFDM_NOISE_REAL) w[j].x = fmaf(sigma, gz.z[j], w[j].x);   // real-only (D7)
+                    for (int j = 0; j < 4; ++j) w[j] = v[u][j];
+                    if (a.noise == OFDM_NOISE_REAL) {   // real-only (D7): sigma z = sqrt(K log2 u1) (cos | sin)
+#ifdef OFDM_FRAME_CAP_VKEYS
+                        const Noise4 nz = noise4_of(po[u], Ksig);
+#else
+                        const Noise4 nz = noise4_of(philox10_c2(hd, (uint32_t)b, a.k0, a.k1), Ksig);
+#endif
+                        w[0].x = fmaf(nz.r0, nz.c0, w[0].x); w[1].x = fmaf(nz.r0, nz.s0, w[1].x);
+                        w[2].x = fmaf(nz.r1, nz.c1, w[2].x); w[3].x = fmaf(nz.r1, nz.s1, w[3].x);
                     }
                     // samples of the block outside [0, L) land in the region's slack, never read as capture
                     float4 *d4 = reinterpret_cast<float4 *>(rbase + 4 * (b - b0));
@@ -501,11 +534,17 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
 
         // ---- Packet_Detection (OFDM.c:659-683): M[n] = |sum r[n+k] r[n+k+16]|^2 / (sum |r[n+k+16]|^2)^2,
         // k < 32, no conjugate, on the UNFILTERED capture; sliding sums over each lane's chunk with the
-        // LDS reads issued 8 positions at a time.  M > 0.75 (OFDM.c:687, 695) is tested as
-        // num > 0.75 den, which keeps the division's 0/0 -> false and x/0 -> true outcomes. ----
+        // LDS reads issued DET_B positions at a time.  M > 0.75 (OFDM.c:687, 695) is decided as the sign
+        // of t = 0.75 den - num (fma: exact before its one rounding): t < 0 <=> crossing, which keeps the
+        // division's outcomes 0/0 -> false (t = +0) and x/0 -> true (t = -num). ----
         const int n0 = tid * chunk, n1 = min(n0 + chunk, Lc);
         unsigned long long cmask = 0ull;            // crossing n at bit n - n0 (chunk <= 64)
+#ifndef FRAME_DET_B
+#define FRAME_DET_B 5
+#endif
+        constexpr int DET_B = FRAME_DET_B;
         if (n0 < n1) {
+#ifdef OFDM_FRAME_DET_OLD      // A/B: products formed, then added (9 VALU per window term, 24 per position)
             float sx = 0.f, sy = 0.f, pw = 0.f;
 #pragma unroll 8
             for (int k = 0; k < 32; ++k) {
@@ -514,29 +553,66 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
                 sy += u.x * v.y + u.y * v.x;
                 pw += v.x * v.x + v.y * v.y;
             }
-            // batches of DET_B positions (the 2961-position capture gives chunks of 25 = 5 x 5); the
-            // batch's crossings are collected with constant shifts and placed once per batch
-#ifndef FRAME_DET_B
-#define FRAME_DET_B 5
-#endif
-            constexpr int DET_B = FRAME_DET_B;
             for (int nb = n0; nb < n1; nb += DET_B) {
                 float2 o0[DET_B], o1[DET_B], i0[DET_B], i1[DET_B];
 #pragma unroll
-                for (int k = 0; k < DET_B; ++k) {       // reads past the capture land in fr/cross: unused
+                for (int k = 0; k < DET_B; ++k) {
                     o0[k] = r[nb + k]; o1[k] = r[nb + k + 16]; i0[k] = r[nb + k + 32]; i1[k] = r[nb + k + 48];
                 }
                 uint32_t m = 0u;
 #pragma unroll
-                for (int k = 0; k < DET_B; ++k) {       // branch-free: positions >= n1 are masked off
+                for (int k = 0; k < DET_B; ++k) {
                     const float num = sx * sx + sy * sy, den = pw * pw;
-                    m |= (nb + k < n1 && num > 0.75f * den) ? 1u << k : 0u;
+                    m |= num > 0.75f * den ? 1u << k : 0u;
                     sx += (i0[k].x * i1[k].x - i0[k].y * i1[k].y) - (o0[k].x * o1[k].x - o0[k].y * o1[k].y);
                     sy += (i0[k].x * i1[k].y + i0[k].y * i1[k].x) - (o0[k].x * o1[k].y + o0[k].y * o1[k].x);
                     pw += (i1[k].x * i1[k].x + i1[k].y * i1[k].y) - (o1[k].x * o1[k].x + o1[k].y * o1[k].y);
                 }
                 cmask |= (unsigned long long)m << (nb - n0);
             }
+#else
+            // every window term accumulated by fma straight into the running sums (6 VALU per term; the
+            // sliding update is 12 fma per position: the entering product added, the leaving one taken off)
+            float sx = 0.f, sy = 0.f, pw = 0.f;
+#pragma unroll 8
+            for (int k = 0; k < 32; ++k) {
+                const float2 u = r[n0 + k], v = r[n0 + k + 16];
+                sx = fmaf(u.x, v.x, sx); sx = fmaf(-u.y, v.y, sx);
+                sy = fmaf(u.x, v.y, sy); sy = fmaf(u.y, v.x, sy);
+                pw = fmaf(v.x, v.x, pw); pw = fmaf(v.y, v.y, pw);
+            }
+            // t's sign bits shifted in with v_alignbit, one per position (first position highest); every
+            // active lane runs the same ceil(chunk / DET_B) batches, positions past n1 are masked below
+            uint32_t mlo = 0u, mhi = 0u;
+            const int nbat = (chunk + DET_B - 1) / DET_B;
+            for (int b = 0; b < nbat; ++b) {
+                const int nb = n0 + DET_B * b;
+                float2 o0[DET_B], o1[DET_B], i0[DET_B], i1[DET_B];
+#pragma unroll
+                for (int k = 0; k < DET_B; ++k) {       // reads past the capture land in the region's slack / cross
+                    o0[k] = r[nb + k]; o1[k] = r[nb + k + 16]; i0[k] = r[nb + k + 32]; i1[k] = r[nb + k + 48];
+                }
+#pragma unroll
+                for (int k = 0; k < DET_B; ++k) {
+                    const float num = fmaf(sx, sx, sy * sy), h = 0.75f * pw;
+                    const float t = fmaf(h, pw, -num);
+                    if (chunk > 32) mhi = __builtin_amdgcn_alignbit(mhi, mlo, 31);
+                    mlo = __builtin_amdgcn_alignbit(mlo, __float_as_uint(t), 31);
+                    sx = fmaf(i0[k].x, i1[k].x, sx); sx = fmaf(-i0[k].y, i1[k].y, sx);
+                    sx = fmaf(-o0[k].x, o1[k].x, sx); sx = fmaf(o0[k].y, o1[k].y, sx);
+                    sy = fmaf(i0[k].x, i1[k].y, sy); sy = fmaf(i0[k].y, i1[k].x, sy);
+                    sy = fmaf(-o0[k].x, o1[k].y, sy); sy = fmaf(-o0[k].y, o1[k].x, sy);
+                    pw = fmaf(i1[k].x, i1[k].x, pw); pw = fmaf(i1[k].y, i1[k].y, pw);
+                    pw = fmaf(-o1[k].x, o1[k].x, pw); pw = fmaf(-o1[k].y, o1[k].y, pw);
+                }
+            }
+            // J = nbat * DET_B positions: position j sits at bit J - 1 - j of (mhi:mlo); reverse the bits
+            const int J = nbat * DET_B;
+            const unsigned long long rev = ((unsigned long long)__builtin_bitreverse32(mlo) << 32) |
+                                           __builtin_bitreverse32(mhi);
+            cmask = rev >> (64 - J);
+#endif
+            if (n1 - n0 < 64) cmask &= (1ull << (n1 - n0)) - 1ull;   // the last batch's positions past n1
             if (cmask) {
                 atomicOr(&cross[n0 >> 6], cmask << (n0 & 63));
                 if ((n0 & 63) + chunk > 64) atomicOr(&cross[(n0 >> 6) + 1], cmask >> (64 - (n0 & 63)));
@@ -590,13 +666,13 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
             fr = off + lo >= nfr ? rbase : rbase + off + hi + 1;
         }
         // ---- RRC matched filter at the down-sampled instants p + 2i (OFDM.c:965, 992-996): outputs
-        // interleaved over the lanes, so a tap's reads are 2 samples apart across lanes (no bank
-        // conflicts); clamped reads + select are Convolution's zero padding ----
+        // interleaved over the lanes, so a tap's reads are 2 samples apart across lanes; clamped reads +
+        // select are Convolution's zero padding.  Only the 160 + 64 nd frame samples the receiver reads
+        // are filtered (needed_k: the coarse-CFO STF lag window, both LTFs, the data windows without
+        // their CPs), all nfr for the single-capture dump.  The OOB flag is unchanged: the reference
+        // reads past its buffer iff the last instant does, and the last sample is always needed. ----
+        const bool dbg = a.dbg_frame && first_item;
         bool oob_l = false;
-#ifndef FRAME_MF_U
-#define FRAME_MF_U 1        // matched-filter outputs per lane per pass (A/B: 2 -> -5 %, 4 -> -24 %: registers)
-#endif
-        constexpr int MF_U = FRAME_MF_U;
         // taps copied to VGPRs: an FMA with an SGPR operand issues in the slow class (+0.6 %)
         float tv[21];
 #ifdef FRAME_TAPS_SGPR
@@ -606,50 +682,39 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
 #pragma unroll
         for (int j = 0; j < 21; ++j) asm volatile("v_mov_b32 %0, %1" : "=v"(tv[j]) : "s"(a.taps[j]));
 #endif
-        // MF_U outputs per lane at once (ii, ii + 128, ...): 2 MF_U independent fma chains instead of 2
-        for (int i0 = tid; i0 < nfr; i0 += MF_U * SYNC_THREADS) {
-            bool inner = true;                                   // every output of the batch interior
+#ifdef OFDM_FRAME_MF_ALL      // A/B: filter every frame sample
+        const int nmf = nfr;
+#else
+        const int nmf = dbg ? nfr : 160 + 64 * a.n_data;
+#endif
+        for (int j = tid; j < nmf; j += SYNC_THREADS) {
+#ifdef OFDM_FRAME_MF_ALL
+            const int ii = j;
+#else
+            const int ii = dbg ? j : needed_k(j);
+#endif
+            const int n = p + 2 * ii;
+            float2 v = make_float2(0.f, 0.f);
+            if (n >= 20 && n < L) {                              // all 21 taps inside the capture
 #pragma unroll
-            for (int u = 0; u < MF_U; ++u) {
-                const int ii = i0 + u * SYNC_THREADS, n = p + 2 * ii;
-                inner = inner && (ii >= nfr || (n >= 20 && n < L));
-            }
-            if (inner) {                                         // all 21 taps inside the capture
-                float2 v[MF_U];
-#pragma unroll
-                for (int u = 0; u < MF_U; ++u) v[u] = make_float2(0.f, 0.f);
-#pragma unroll
-                for (int j = 0; j < 21; ++j)
-#pragma unroll
-                    for (int u = 0; u < MF_U; ++u) {
-                        // outputs past nfr read inside the region (n - j < L) and are not stored
-                        const float2 x = r[min(p + 2 * (i0 + u * SYNC_THREADS), L - 1) - j];
-                        v[u].x = fmaf(x.x, tv[j], v[u].x);
-                        v[u].y = fmaf(x.y, tv[j], v[u].y);
-                    }
-#pragma unroll
-                for (int u = 0; u < MF_U; ++u)
-                    if (i0 + u * SYNC_THREADS < nfr) fr[i0 + u * SYNC_THREADS] = v[u];   // outside every lane's reads
+                for (int t = 0; t < 21; ++t) {
+                    const float2 x = r[n - t];
+                    v.x = fmaf(x.x, tv[t], v.x);
+                    v.y = fmaf(x.y, tv[t], v.y);
+                }
+            } else if (n >= L + 20) {
+                oob_l = true;                                    // the reference reads past its buffer
             } else {
-                for (int u = 0; u < MF_U; ++u) {
-                    const int ii = i0 + u * SYNC_THREADS, n = p + 2 * ii;
-                    if (ii >= nfr) break;
-                    float2 v = make_float2(0.f, 0.f);
-                    if (n >= L + 20) {
-                        oob_l = true;                            // the reference reads past its buffer
-                    } else {
 #pragma unroll
-                        for (int j = 0; j < 21; ++j) {
-                            const int m = n - j;
-                            float2 x = r[min(max(m, 0), L - 1)];
-                            x = (m >= 0 && m < L) ? x : make_float2(0.f, 0.f);
-                            v.x = fmaf(x.x, tv[j], v.x);
-                            v.y = fmaf(x.y, tv[j], v.y);
-                        }
-                    }
-                    fr[ii] = v;
+                for (int t = 0; t < 21; ++t) {
+                    const int m = n - t;
+                    float2 x = r[min(max(m, 0), L - 1)];
+                    x = (m >= 0 && m < L) ? x : make_float2(0.f, 0.f);
+                    v.x = fmaf(x.x, tv[t], v.x);
+                    v.y = fmaf(x.y, tv[t], v.y);
                 }
             }
+            fr[ii] = v;                                          // outside every lane's reads
         }
         const bool oob = block_max_i(oob_l ? 1 : 0, redi) != 0;   // also orders fr[] for every lane
         FR_STAMP(3);                                           // matched filter + down-sample
@@ -681,24 +746,28 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
         // 1024-1040) ----
         const int nw = 2 + a.n_data;
         float2 *dst = a.win + i * (int64_t)(nw * 64);
-        const bool dbg = a.dbg_frame && first_item;
 #ifndef OFDM_FRAME_CFO_TWO_STEP
         const double fcf_ts = (fc + ff) * TS;
 #endif
-        for (int k = tid; k < nfr; k += SYNC_THREADS) {
+        // hand-off sample j = window j / 64, sample j % 64 (contiguous stores); the dump rotates all nfr
+        const int nrot = dbg ? nfr : 64 * nw;
+        for (int j = tid; j < nrot; j += SYNC_THREADS) {
+            int k = needed_k(j + 32), w = j >> 6, n = j & 63;
+            if (dbg) {
+                k = j; w = -1;
+                if (k >= 192 && k < 320) {
+                    w = (k - 192) >> 6; n = (k - 192) & 63;
+                } else if (k >= 336) {
+                    const int d = (k - 336) / 80, o = k - 336 - 80 * d;
+                    if (d < a.n_data && o < 64) { w = 2 + d; n = o; }
+                }
+            }
 #ifdef OFDM_FRAME_CFO_TWO_STEP
             const float2 v = cfo_rot(cfo_rot(fr[k], fc * TS, k), ff * TS, k);
 #else
             const float2 v = cfo_rot(fr[k], fcf_ts, k);
 #endif
             if (dbg) a.dbg_frame[k] = v;
-            int w = -1, n = 0;
-            if (k >= 192 && k < 320) {
-                w = (k - 192) >> 6; n = (k - 192) & 63;
-            } else if (k >= 336) {
-                const int d = (k - 336) / 80, o = k - 336 - 80 * d;
-                if (d < a.n_data && o < 64) { w = 2 + d; n = o; }
-            }
             if (w >= 0) dst[w * 64 + n] = v;
         }
         FR_STAMP(4);                                           // coarse + fine CFO + hand-off
