@@ -202,16 +202,34 @@ __device__ __forceinline__ float wave_sum_f(float v) {
            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)) +
            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
 }
-__device__ __forceinline__ int wave_max_i(int v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+// wave-uniform max / min of an int: DPP within each row of 16 lanes (quad xor 1, xor 2, half-row and
+// row mirrors), then the four row results by readlane -- no LDS round trips (a __shfl_xor ladder is six
+// serial ds_bpermute)
+template <bool MAX>
+__device__ __forceinline__ int wave_ext_i(int v) {
+    auto f = [](int a, int b) { return MAX ? max(a, b) : min(a, b); };
+    v = f(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false));
+    v = f(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false));
+    v = f(v, __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, false));
+    v = f(v, __builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, false));
+    return f(f(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+             f(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+}
+__device__ __forceinline__ int wave_max_i(int v) { return wave_ext_i<true>(v); }
+__device__ __forceinline__ int wave_min_i(int v) { return wave_ext_i<false>(v); }
+// inclusive prefix max over the wave's lanes (v >= -1): row_shr 1, 2, 4, 8 within each row, then
+// row_bcast 15 / 31 carry row results into the later rows; lanes without a source keep -1
+__device__ __forceinline__ int wave_prefix_max(int v) {
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x111, 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x112, 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x114, 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x118, 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x142, 0xA, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x143, 0xC, 0xF, false));
     return v;
 }
-__device__ __forceinline__ int wave_min_i(int v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
-    return v;
-}
+// the previous lane's value (-1 for lane 0): DPP wave_shr:1
+__device__ __forceinline__ int wave_shr1(int v) { return __builtin_amdgcn_update_dpp(-1, v, 0x138, 0xF, 0xF, false); }
 
 __device__ __forceinline__ float wave_min_f(float v) {
 #pragma unroll
@@ -639,6 +657,7 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
         // first crossing can be one, and its predecessor is the last crossing of the earlier chunks:
         // an exclusive prefix max over the block's lanes.  The first front x with a later front and
         // M[front+230] > 0.75 gives packet_idx = front + len_RRC_rx + 1; otherwise 0 (OFDM.c:752-761). ----
+#ifdef OFDM_FRAME_SCAN_SHFL     // A/B: the ds_bpermute ladder
         int pm = last;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -647,6 +666,10 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
         }
         int prev = __shfl_up(pm, 1, 64);
         if (lane == 0) prev = -1;
+#else
+        const int pm = wave_prefix_max(last);
+        int prev = wave_shr1(pm);
+#endif
         if (lane == 63) redi[RED_I_PREFIX + (tid >> 6)] = pm;   // each wave's last crossing
         __syncthreads();                            // crossing words and wave prefixes are in LDS
         for (int w = 0; w < (tid >> 6); ++w) prev = max(prev, redi[RED_I_PREFIX + w]);   // earlier waves
@@ -696,11 +719,34 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
             const int n = p + 2 * ii;
             float2 v = make_float2(0.f, 0.f);
             if (n >= 20 && n < L) {                              // all 21 taps inside the capture
+#ifdef OFDM_FRAME_MF_B64      // A/B: one ds_read_b64 per tap (lanes 16 B apart: 2-way bank conflicts)
+                float2 x[21];
+#pragma unroll
+                for (int t = 0; t < 21; ++t) x[t] = r[n - t];
+#else
+                // samples n-20 .. n as 10 sample pairs + 1 single: a ds_read_b128 per pair, 16-byte
+                // aligned in the region (rbase); lanes read adjacent 16 B (conflict-free).  The pairs start
+                // at n-20 or n-19 depending on the parity of the region index, uniform per item.
+                float2 x[21];                                    // x[t] = sample n - t
+                const int s0 = n - 20 + (rx_start & 3);          // region index of sample n - 20
+                auto load = [&](auto oc) {
+                    constexpr int ODD = decltype(oc)::value;
+                    const float4 *q4 = reinterpret_cast<const float4 *>(rbase + s0 + ODD);
+#pragma unroll
+                    for (int m = 0; m < 10; ++m) {
+                        const float4 w = q4[m];                  // samples n-20+ODD+2m, n-19+ODD+2m
+                        x[20 - ODD - 2 * m] = make_float2(w.x, w.y);
+                        x[19 - ODD - 2 * m] = make_float2(w.z, w.w);
+                    }
+                    x[ODD ? 20 : 0] = rbase[ODD ? s0 : s0 + 20];  // the sample the pairs leave out
+                };
+                if (s0 & 1) load(std::integral_constant<int, 1>{});
+                else load(std::integral_constant<int, 0>{});
+#endif
 #pragma unroll
                 for (int t = 0; t < 21; ++t) {
-                    const float2 x = r[n - t];
-                    v.x = fmaf(x.x, tv[t], v.x);
-                    v.y = fmaf(x.y, tv[t], v.y);
+                    v.x = fmaf(x[t].x, tv[t], v.x);
+                    v.y = fmaf(x[t].y, tv[t], v.y);
                 }
             } else if (n >= L + 20) {
                 oob_l = true;                                    // the reference reads past its buffer
@@ -716,29 +762,38 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
             }
             fr[ii] = v;                                          // outside every lane's reads
         }
-        const bool oob = block_max_i(oob_l ? 1 : 0, redi) != 0;   // also orders fr[] for every lane
+        // each wave's OOB flag, read by thread 0 after the barrier that also orders fr[] for every lane
+        if (lane == 0) redi[RED_I_MAX + (tid >> 6)] = __ballot(oob_l) != 0ull;
+        __syncthreads();
         FR_STAMP(3);                                           // matched filter + down-sample
 
-        // ---- Coarse CFO (OFDM.c:773-804): 16-lag autocorrelation of the short preamble ----
-        float2 pp = make_float2(0.f, 0.f);
-        if (tid < 16) {
-            const float2 u = fr[80 + tid], v = fr[96 + tid];
-            pp = make_float2(u.x * v.x + u.y * v.y, u.y * v.x - u.x * v.y);
-        }
-        pp = block_sum_f2(pp, redf);
-        double fc = (-1.0 / (2.0 * M_PI * 16.0 * TS)) * (double)atan2f(pp.y, pp.x);
-        if (a.float_cfo) fc = (double)(float)fc;
-        // ---- Fine CFO (OFDM.c:806-828): 64-lag over the two long training symbols after the coarse
-        // rotation; the 128 rotated LTF samples are formed on the fly (the same arithmetic as rotating
-        // the whole frame first) ----
-        pp = make_float2(0.f, 0.f);
+        // ---- Coarse CFO (OFDM.c:773-804): 16-lag autocorrelation of the short preamble; fine CFO
+        // (OFDM.c:806-828): 64-lag over the two long training symbols after the coarse rotation, the 128
+        // rotated LTF samples formed on the fly (the same arithmetic as rotating the whole frame first).
+        // Wave 0 holds every term: both estimates are wave reductions there, and one barrier hands the
+        // frequencies to the other waves. ----
+        double *cfo_sh = reinterpret_cast<double *>(redf);      // [fc, ff]
         if (tid < 64) {
+            float2 pp = make_float2(0.f, 0.f);
+            if (tid < 16) {
+                const float2 u = fr[80 + tid], v = fr[96 + tid];
+                pp = make_float2(u.x * v.x + u.y * v.y, u.y * v.x - u.x * v.y);
+            }
+            pp.x = wave_sum_f(pp.x);
+            pp.y = wave_sum_f(pp.y);
+            double fc = (-1.0 / (2.0 * M_PI * 16.0 * TS)) * (double)atan2f(pp.y, pp.x);
+            if (a.float_cfo) fc = (double)(float)fc;
             const float2 u = cfo_rot(fr[192 + tid], fc * TS, 192 + tid), v = cfo_rot(fr[256 + tid], fc * TS, 256 + tid);
             pp = make_float2(u.x * v.x + u.y * v.y, u.y * v.x - u.x * v.y);
+            pp.x = wave_sum_f(pp.x);
+            pp.y = wave_sum_f(pp.y);
+            double ff = (-1.0 / (2.0 * M_PI * 64.0 * TS)) * (double)atan2f(pp.y, pp.x);
+            if (a.float_cfo) ff = (double)(float)ff;
+            if (tid == 0) { cfo_sh[0] = fc; cfo_sh[1] = ff; }
         }
-        pp = block_sum_f2(pp, redf);
-        double ff = (-1.0 / (2.0 * M_PI * 64.0 * TS)) * (double)atan2f(pp.y, pp.x);
-        if (a.float_cfo) ff = (double)(float)ff;
+        __syncthreads();
+        const double fc = cfo_sh[0], ff = cfo_sh[1];
+        (void)fc; (void)ff;
         // ---- coarse then fine rotation (OFDM.c:802, 825) as ONE rotation by the summed phase
         // 2 pi (fc + ff) Ts k, evaluated in fp64 revolutions (the reference's two double-precision
         // cexp products rounded to float twice; the same rotation to fp32 rounding), the result handed
@@ -772,6 +827,9 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
         }
         FR_STAMP(4);                                           // coarse + fine CFO + hand-off
         if (tid == 0) {
+            int oob = 0;
+#pragma unroll
+            for (int w = 0; w < SYNC_WAVES; ++w) oob |= redi[RED_I_MAX + w];
             a.info[i] = make_int4(p, sync_fail, oob, rx_start);
             unsigned long long *sl = acc + q * ACC_SLOTS;
             sl[3] += sync_fail;
