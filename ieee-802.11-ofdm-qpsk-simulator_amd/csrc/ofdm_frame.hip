@@ -426,6 +426,15 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
         opaque(tid);
         const int lane = tid & 63;
 #endif
+#ifndef FRAME_HOIST_ARGS
+        // the kernel arguments are re-read per item (scalar loads from the kernarg segment through a pointer
+        // made opaque here) instead of being hoisted into ~100 SGPRs held across the item loop, most of
+        // which spilled to VGPR lanes and came back by v_readlane (a VALU op) at every use
+        using KArgs = const __attribute__((address_space(4))) FrameArgs;
+        KArgs *ap = (KArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(ap));
+        KArgs &a = *ap;
+#endif
         const int64_t g = a.item0 + i;
         int q;
         int64_t ti;
@@ -702,8 +711,18 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
 #pragma unroll
         for (int j = 0; j < 21; ++j) tv[j] = a.taps[j];
 #else
+        {
+            // read from the kernarg segment through a pointer made opaque per item, so the 21 taps are
+            // scalar-loaded here and die at the copy instead of being hoisted into SGPRs held across the
+            // item loop (they were most of the loop's SGPR spills)
+            using kchar = __attribute__((address_space(4))) char;
+            using kfloat = __attribute__((address_space(4))) float;
+            const kfloat *tp = (const kfloat *)((const kchar *)__builtin_amdgcn_kernarg_segment_ptr() +
+                                                    offsetof(FrameArgs, taps));
+            asm volatile("" : "+s"(tp));
 #pragma unroll
-        for (int j = 0; j < 21; ++j) asm volatile("v_mov_b32 %0, %1" : "=v"(tv[j]) : "s"(a.taps[j]));
+            for (int j = 0; j < 21; ++j) asm volatile("v_mov_b32 %0, %1" : "=v"(tv[j]) : "s"(tp[j]));
+        }
 #endif
 #ifdef OFDM_FRAME_MF_ALL      // A/B: filter every frame sample
         const int nmf = nfr;

@@ -2,5 +2,5 @@ set -u
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_gpu_frame.py tests/test_gpu_message.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/frame_tests.log 2>&1; rc=$?; echo "frame tests rc=$rc"; tail -3 gpurun_out/frame_tests.log
 [ $rc -ge 2 ] && exit $rc
-SYMBOLS=1000000 VARIANTS="default mf_b64 scan_shfl default stamps" WORKLOADS="frame" bash tools/ab.sh
-grep "frame stamp" gpurun_out/ab_frame_stamps.err | head -8
+SYMBOLS=1000000 VARIANTS="default hoist_args default stamps" WORKLOADS="frame" bash tools/ab.sh
+grep "frame stamp" gpurun_out/ab_frame_stamps.err | head -7
