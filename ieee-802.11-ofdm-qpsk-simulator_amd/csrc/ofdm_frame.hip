@@ -369,11 +369,14 @@ __device__ __forceinline__ int block_max_i(int v, int *red) {
     for (int w = 1; w < SYNC_WAVES; ++w) t = max(t, red[w]);
     return t;
 }
-// (min of a, max of b) over the waves in one exchange (scratch: 2 SYNC_WAVES slots)
+// (min of a, max of b) over the waves in one exchange (scratch: 2 SYNC_WAVES slots).  LEAD: the barrier
+// that keeps the slots from being overwritten while an earlier exchange still reads them; the item
+// loop's slots were last read before the previous item's closing barrier, so it passes false.
+template <bool LEAD = true>
 __device__ __forceinline__ int2 block_minmax_i(int a, int b, int *red) {
     a = wave_min_i(a);
     b = wave_max_i(b);
-    __syncthreads();
+    if (LEAD) __syncthreads();
     if ((threadIdx.x & 63) == 0) { red[2 * (threadIdx.x >> 6)] = a; red[2 * (threadIdx.x >> 6) + 1] = b; }
     __syncthreads();
     int2 t = make_int2(red[0], red[1]);
@@ -686,7 +689,11 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
         FR_STAMP(1);                                           // packet detection
         const bool valid = front >= 0 && front + 230 < Lc && bit_at(cross, front + 230);
         // the first valid front that has a later front: the least valid front, unless it is the last one
-        const int2 mm = block_minmax_i(valid ? front : 0x7fffffff, front, redi + RED_I_MINMAX);
+#ifdef OFDM_FRAME_MINMAX_LEAD   // A/B: the leading barrier kept
+        const int2 mm = block_minmax_i<true>(valid ? front : 0x7fffffff, front, redi + RED_I_MINMAX);
+#else
+        const int2 mm = block_minmax_i<false>(valid ? front : 0x7fffffff, front, redi + RED_I_MINMAX);
+#endif
         const int cand = mm.x < mm.y ? mm.x : 0x7fffffff;
         const bool sync_fail = cand == 0x7fffffff;
         const int p = sync_fail ? 0 : cand + 10 + 1;           // len_RRC_rx + 1 (OFDM.c:758)

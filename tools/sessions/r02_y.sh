@@ -1,0 +1,7 @@
+set -u
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_frame.py tests/test_gpu_message.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/frame_tests.log 2>&1; rc=$?; echo "frame tests rc=$rc"; tail -3 gpurun_out/frame_tests.log
+[ $rc -ge 2 ] && exit $rc
+OFDM_MI355X_LIB=variants/libofdm_det64.so timeout -k 10 300 python -u -m pytest tests/test_gpu_frame.py tests/test_gpu_message.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/frame_tests_det64.log 2>&1; rc=$?; echo "det64 frame tests rc=$rc"; tail -3 gpurun_out/frame_tests_det64.log
+[ $rc -ge 2 ] && exit $rc
+SYMBOLS=1000000 VARIANTS="default lead det64 default" WORKLOADS="frame" bash tools/ab.sh
