@@ -2,14 +2,16 @@
 //
 //   K4a frame_wave_kernel : Transmitter() (OFDM.c:467-618) -- preambles + data symbols, 2x zero
 //                           stuffing, 21-tap RRC, x10 repeat, mean power (OFDM.c:637-643).
-//   K4b frame_rx_kernel   : one wave per trial: capture (OFDM.c:945-955) + real AWGN (OFDM.c:651),
-//                           Packet_Detection (659-683) with sliding sums, Packet_Selection (685-771)
-//                           as a wave ballot/min, RRC matched filter evaluated only at the 320+80D
-//                           down-sampled instants (965, 984-996), coarse/fine CFO (773-828), then the
-//                           same register FFT + LS estimate + demap as symbol mode (830-1165).
+//   K4b frame_sync_kernel : one 128-thread block per (trial, SNR) item: capture (OFDM.c:945-955) + real
+//                           AWGN (OFDM.c:651) in LDS, Packet_Detection (659-683) as fma-chained sliding
+//                           sums with sign-bit crossings, Packet_Selection (685-771) as a DPP prefix max
+//                           + block min/max, the RRC matched filter only at the down-sampled instants the
+//                           receiver reads (965, 984-996), coarse/fine CFO (773-828) on wave 0, and the
+//                           rotated LTF / data windows handed to
+//   K4b' frame_sym_kernel : the same register FFT + LS estimate + demap as symbol mode (830-1165).
 //   K4c ota_kernel        : Transmission_Over_Air() on a caller-provided waveform.
 //
-// The capture lives in LDS (24 KB per wave for the reference's 2-symbol message; frames carry 1..8
+// The capture lives in LDS (24 KB per trial for the reference's 2-symbol message; frames carry 1..8
 // data symbols, ofdm_set_message); detection keeps only the >0.75 crossings as a bit mask, since
 // Packet_Selection needs nothing else (it re-reads Corr_Out only at front+230).
 #include "ofdm_internal.h"
