@@ -193,9 +193,13 @@ int ofdm_ctx_destroy(ofdm_ctx *ctx) {
     for (auto &e : c->done) { hipEventDestroy(e.a); hipEventDestroy(e.b); }
     for (auto &e : c->open) { hipEventDestroy(e.a); hipEventDestroy(e.b); }
     for (auto ev : c->pool) hipEventDestroy(ev);
+    if (c->tx_stream) hipStreamSynchronize(c->tx_stream);
     for (void *p : {(void *)c->d_ltf[0], (void *)c->d_ltf[1], (void *)c->d_ltf2_rows[0], (void *)c->d_ltf2_rows[1], c->d_tx, c->d_bits, c->d_cnt, c->d_scratch,
-                    c->d_scratch2, c->d_wave})
+                    c->d_scratch2, c->d_wave, c->d_tx2, c->d_bits2})
         if (p) hipFree(p);
+    for (hipEvent_t ev : {c->ev_start, c->ev_tx[0], c->ev_tx[1], c->ev_rx[0], c->ev_rx[1]})
+        if (ev) hipEventDestroy(ev);
+    if (c->tx_stream) hipStreamDestroy(c->tx_stream);
     if (c->own) hipStreamDestroy(c->own);
     delete c;
     return OFDM_OK;
@@ -398,17 +402,53 @@ int ofdm_symbol_sweep(ofdm_ctx *ctx, const ofdm_cfg *cfg, const double *snr_db, 
     const size_t cbytes = (size_t)n_snr * OFDM_NCOUNTERS * sizeof(int64_t);
     if ((rc = c->ensure(&c->d_cnt, &c->cap_cnt, cbytes))) return rc;
     HIPOK(hipMemsetAsync(c->d_cnt, 0, cbytes, c->stream));
-    if (chunk_frames <= 0) chunk_frames = int64_t(1) << 22;           // 8.4M symbols, ~5.4 GB per chunk
+    if (chunk_frames <= 0) {
+        // 8.4M symbols (~5.4 GB) per chunk, and at least SWEEP_PIPE chunks of >= 2^18 frames, so that the
+        // HBM-bound Tx of chunk k+1 runs on the context's second stream under the VALU-bound receiver of
+        // chunk k (double-buffered batches; the counters do not depend on the chunking)
+        chunk_frames = int64_t(1) << 22;
+        constexpr int64_t SWEEP_PIPE = 4, MIN_PIPE = int64_t(1) << 18;
+        if (n_frames >= SWEEP_PIPE * MIN_PIPE) chunk_frames = std::min(chunk_frames, (n_frames + SWEEP_PIPE - 1) / SWEEP_PIPE);
+    }
     chunk_frames = std::min(chunk_frames, MAX_BATCH_FRAMES);
     const int64_t cf = std::min<int64_t>(chunk_frames, std::max<int64_t>(n_frames, 1));
+    const int64_t n_chunks = (n_frames + cf - 1) / cf;
     int64_t txb = 0, bb = 0;
     ofdm_tx_bytes(cf, &txb, &bb);
     if ((rc = c->ensure(&c->d_tx, &c->cap_tx, (size_t)txb))) return rc;
     if ((rc = c->ensure(&c->d_bits, &c->cap_bits, (size_t)bb))) return rc;
-    for (int64_t done = 0; done < n_frames; done += cf) {
-        const int64_t nf = std::min(cf, n_frames - done);
-        if ((rc = ofdm_tx_frames(ctx, cfg, first_frame + done, nf, c->d_tx, c->d_bits))) return rc;
-        if ((rc = ofdm_rx_frames(ctx, cfg, c->d_tx, c->d_bits, first_frame + done, nf, snr_db, n_snr, c->d_cnt))) return rc;
+    if (n_chunks > 1) {
+        if ((rc = c->ensure(&c->d_tx2, &c->cap_tx2, (size_t)txb))) return rc;
+        if ((rc = c->ensure(&c->d_bits2, &c->cap_bits2, (size_t)bb))) return rc;
+        if (!c->tx_stream) HIPOK(hipStreamCreateWithFlags(&c->tx_stream, hipStreamNonBlocking));
+        for (hipEvent_t *ev : {&c->ev_start, &c->ev_tx[0], &c->ev_tx[1], &c->ev_rx[0], &c->ev_rx[1]})
+            if (!*ev) HIPOK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+        HIPOK(hipEventRecord(c->ev_start, c->stream));          // the Tx stream starts after the memset
+        HIPOK(hipStreamWaitEvent(c->tx_stream, c->ev_start, 0));
+    }
+    float2 *txbuf[2] = {(float2 *)c->d_tx, (float2 *)c->d_tx2};
+    uint32_t *bitbuf[2] = {(uint32_t *)c->d_bits, (uint32_t *)c->d_bits2};
+    hipStream_t main_stream = c->stream;
+    auto chunk_of = [&](int64_t k, int64_t *first, int64_t *nf) { *first = first_frame + k * cf; *nf = std::min(cf, n_frames - k * cf); };
+    int64_t f0, n0;
+    chunk_of(0, &f0, &n0);
+    if ((rc = ofdm_tx_frames(ctx, cfg, f0, n0, txbuf[0], bitbuf[0]))) return rc;
+    for (int64_t k = 0; k < n_chunks; ++k) {
+        if (k + 1 < n_chunks) {                                  // Tx of chunk k+1 into the other batch
+            if (k >= 1) HIPOK(hipStreamWaitEvent(c->tx_stream, c->ev_rx[(k - 1) & 1], 0));   // chunk k-1 read it
+            int64_t f1, n1;
+            chunk_of(k + 1, &f1, &n1);
+            c->stream = c->tx_stream;
+            rc = ofdm_tx_frames(ctx, cfg, f1, n1, txbuf[(k + 1) & 1], bitbuf[(k + 1) & 1]);
+            c->stream = main_stream;
+            if (rc) return rc;
+            HIPOK(hipEventRecord(c->ev_tx[(k + 1) & 1], c->tx_stream));
+        }
+        if (k >= 1) HIPOK(hipStreamWaitEvent(main_stream, c->ev_tx[k & 1], 0));
+        int64_t fk, nk;
+        chunk_of(k, &fk, &nk);
+        if ((rc = ofdm_rx_frames(ctx, cfg, txbuf[k & 1], bitbuf[k & 1], fk, nk, snr_db, n_snr, c->d_cnt))) return rc;
+        if (n_chunks > 1) HIPOK(hipEventRecord(c->ev_rx[k & 1], main_stream));
     }
     HIPOK(hipMemcpyAsync(counters, c->d_cnt, cbytes, hipMemcpyDeviceToHost, c->stream));
     HIPOK(hipStreamSynchronize(c->stream));

@@ -28,6 +28,11 @@ struct Ctx {
     std::string message = "Hey! I am Vivaswan";   // MESSAGE payload (OFDM.c:20), ofdm_set_message
     // sweep scratch (grown on demand, freed with the context)
     void *d_tx = nullptr, *d_bits = nullptr, *d_cnt = nullptr, *d_scratch = nullptr, *d_scratch2 = nullptr;
+    // ofdm_symbol_sweep's pipeline: the second Tx batch and the stream the next chunk's Tx runs on
+    void *d_tx2 = nullptr, *d_bits2 = nullptr;
+    size_t cap_tx2 = 0, cap_bits2 = 0;
+    hipStream_t tx_stream = nullptr;
+    hipEvent_t ev_start = nullptr, ev_tx[2] = {nullptr, nullptr}, ev_rx[2] = {nullptr, nullptr};
     void *d_wave = nullptr;
     size_t cap_tx = 0, cap_bits = 0, cap_cnt = 0, cap_scratch = 0, cap_scratch2 = 0, cap_wave = 0;
     // frame-mode waveform cache (per conv/payload/message)
