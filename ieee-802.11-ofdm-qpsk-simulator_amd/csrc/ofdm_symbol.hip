@@ -182,6 +182,87 @@ __global__ __launch_bounds__(256) void fft64_wave_kernel(const float2 *__restric
     }
 }
 
+// K1 as launched: FOUR LANES (a quad) PER TRANSFORM.  Lane q of the quad loads the 16 contiguous samples
+// x[16q + j] (128 B: eight 16-byte loads), then
+//   X[4k + r] = sum_j W16^{jk} ( W64^{jr} sum_q x[16q + j] W4^{qr} )     (radix-4 DIF, first stage across lanes)
+// the inner 4-point DFT over q runs across the quad as two DPP exchanges (quad_perm xor 2, xor 1), lane q
+// ending with output residue r = bitrev2(q); the twiddles W64^{jr} are per-lane constants held in VGPRs;
+// the 16-point DFT over j runs in the lane's registers (dif4<16>).  No LDS, ~29 VALU wave-instructions
+// per transform against the wavefront mapping's 70 + 24 ds_bpermute, so the kernel is HBM-bound.
+#ifndef OFDM_K1_QUAD_T
+#define OFDM_K1_QUAD_T 1    // transforms per quad with their loads in flight together (A/B: 2 -2 %, 4 -5 %)
+#endif
+template <int CTRL>
+__device__ __forceinline__ float2 dpp_f2(float2 v) {
+    return make_float2(__int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v.x), CTRL, 0xF, 0xF, false)),
+                       __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v.y), CTRL, 0xF, 0xF, false)));
+}
+template <bool INV, int CONV>
+__global__ __launch_bounds__(256) void fft64_quad_kernel(const float2 *__restrict__ in, float2 *__restrict__ out,
+                                                         int64_t n) {
+    constexpr int T = OFDM_K1_QUAD_T;
+    const int q = threadIdx.x & 3;
+    const int r = ((q & 1) << 1) | (q >> 1);                      // output residue of this lane
+    const int64_t t0 = ((int64_t)blockIdx.x * 64 + (threadIdx.x >> 2)) * T;
+    // per-lane constants: stage-1 sign, stage-2 coefficients (own * a + partner * b, a, b in {+-1, +-j}),
+    // twiddles W64^{jr} (forward e^{-j...}, inverse e^{+j...}) selected from the exact constant table
+    const float s1 = q < 2 ? 1.0f : -1.0f;
+    const float jf = INV ? -1.0f : 1.0f;                          // -j (forward) / +j (inverse) = jf * (-j)
+    const float2 ca = q == 3 ? make_float2(0.f, jf) : make_float2(q == 1 ? -1.0f : 1.0f, 0.f);
+    const float2 cb = q == 2 ? make_float2(0.f, -jf) : make_float2(1.0f, 0.f);
+    float2 tw[16];
+    static_for<1, 16>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        auto w = [](auto ec) {
+            constexpr int e = decltype(ec)::value % 64;
+            return make_float2(kCos64[e], INV ? kSin64[e] : -kSin64[e]);
+        };
+        const float2 w1 = w(std::integral_constant<int, j>{}), w2 = w(std::integral_constant<int, 2 * j>{}),
+                     w3 = w(std::integral_constant<int, 3 * j>{});
+        tw[j] = r == 1 ? w1 : r == 2 ? w2 : w3;                  // r == 0 lanes: j's twiddle is 1, see below
+        if (r == 0) tw[j] = make_float2(1.0f, 0.0f);
+    });
+    const float out_scale = INV ? ((r & 1) ? -1.0f / 64.0f : 1.0f / 64.0f) : 1.0f;   // bin parity = r parity
+    float2 x[T][64];                                              // x[u][j], j < 16 used
+#pragma unroll
+    for (int u = 0; u < T; ++u) {
+        const int64_t t = t0 + u;
+        const float4 *src = reinterpret_cast<const float4 *>(in + (t < n ? t : 0) * 64 + 16 * q);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const float4 v = t < n ? src[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+            x[u][2 * c] = make_float2(v.x, v.y);
+            x[u][2 * c + 1] = make_float2(v.z, v.w);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < T; ++u) {
+        const int64_t t = t0 + u;
+        static_for<0, 16>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            // (-1)^n input modulation (n = 16q + j: the parity of j), D5
+            constexpr float sg = ((!INV || CONV == OFDM_CONV_C) && (j & 1)) ? -1.0f : 1.0f;
+            float2 v = make_float2(sg * x[u][j].x, sg * x[u][j].y);
+            const float2 p2 = dpp_f2<DPP_QUAD_XOR2>(v);           // stage 1: t = s1 own + partner
+            v = make_float2(fmaf(s1, v.x, p2.x), fmaf(s1, v.y, p2.y));
+            const float2 p1 = dpp_f2<DPP_QUAD_XOR1>(v);           // stage 2: a own + b partner
+            v = make_float2(ca.x * v.x - ca.y * v.y + (cb.x * p1.x - cb.y * p1.y),
+                            ca.x * v.y + ca.y * v.x + (cb.x * p1.y + cb.y * p1.x));
+            if constexpr (j > 0) v = make_float2(fmaf(v.x, tw[j].x, -v.y * tw[j].y), fmaf(v.x, tw[j].y, v.y * tw[j].x));
+            x[u][j] = v;
+        });
+        dif4<INV, 16, 0>(x[u]);                                   // bin k' at position rev16(k')
+        if (t < n) {
+            float2 *dst = out + t * 64 + r;
+            static_for<0, 16>([&](auto pc) {
+                constexpr int pos = decltype(pc)::value;
+                constexpr int kp = ((pos & 3) << 2) | (pos >> 2);   // rev16 is its own inverse
+                dst[4 * kp] = cscale(x[u][pos], out_scale);
+            });
+        }
+    }
+}
+
 // ======================================================================== K2: Tx builder
 // One lane = one data symbol: bits -> QPSK (OFDM.c:415-433) -> subcarrier map + pilots
 // (OFDM.c:523-548) -> ifft (OFDM.c:320-339, convention D5) -> CP (OFDM.c:559-565) -> HBM.
@@ -788,7 +869,12 @@ __global__ __launch_bounds__(256, OFDM_RX_IDEAL_WAVES) void rx_ideal_kernel(RxAr
 // ======================================================================== launchers
 template <bool INV>
 static void launch_fft_conv(int conv, dim3 g, hipStream_t st, const float2 *in, float2 *out, int64_t n) {
-#ifndef OFDM_K1_LANE
+#if !defined(OFDM_K1_LANE) && !defined(OFDM_K1_WAVE)
+    const dim3 gq((unsigned)((n + 64 * OFDM_K1_QUAD_T - 1) / (64 * OFDM_K1_QUAD_T)));
+    if (conv == OFDM_CONV_C) hipLaunchKernelGGL((fft64_quad_kernel<INV, OFDM_CONV_C>), gq, dim3(256), 0, st, in, out, n);
+    else hipLaunchKernelGGL((fft64_quad_kernel<INV, OFDM_CONV_MATLAB>), gq, dim3(256), 0, st, in, out, n);
+    (void)g;
+#elif !defined(OFDM_K1_LANE)    // A/B: one transform per wavefront
     const dim3 gw((unsigned)((n + 4 * OFDM_K1_WAVE_T - 1) / (4 * OFDM_K1_WAVE_T)));
     if (conv == OFDM_CONV_C) hipLaunchKernelGGL((fft64_wave_kernel<INV, OFDM_CONV_C>), gw, dim3(256), 0, st, in, out, n);
     else hipLaunchKernelGGL((fft64_wave_kernel<INV, OFDM_CONV_MATLAB>), gw, dim3(256), 0, st, in, out, n);

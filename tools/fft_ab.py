@@ -1,7 +1,7 @@
 """K1 throughput (batched 64-point fft / ifft through ofdm_fft64), for the mapping A/B of DESIGN.md §4.
 
 usage: [OFDM_MI355X_LIB=variants/libofdm_X.so] python tools/fft_ab.py [n_transforms]
-Prints transforms/s and the HBM rate (1 KB in + 1 KB out per transform) from the HIP-event kernel time."""
+Prints transforms/s and the HBM rate (512 B in + 512 B out per transform) from the HIP-event kernel time."""
 import json
 import sys
 from pathlib import Path
