@@ -338,39 +338,7 @@ __host__ __device__ inline size_t frame_lds_bytes(int cap_len, int n_data, int n
            RED_WORDS * 4 + (in_cap ? 0 : (size_t)fr_len(n_data) * 8);
 }
 
-// block-wide reductions over the SYNC_WAVES waves, the wave partials combined in wave order
-__device__ __forceinline__ float block_sum_f(float v, float *red) {
-    v = wave_sum_f(v);
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-    __syncthreads();
-    float t = red[0];
-#pragma unroll
-    for (int w = 1; w < SYNC_WAVES; ++w) t += red[w];
-    return t;
-}
-// the sum of a float pair (scratch: 2 SYNC_WAVES slots), in the same order as block_sum_f
-__device__ __forceinline__ float2 block_sum_f2(float2 v, float *red) {
-    v.x = wave_sum_f(v.x);
-    v.y = wave_sum_f(v.y);
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) { red[2 * (threadIdx.x >> 6)] = v.x; red[2 * (threadIdx.x >> 6) + 1] = v.y; }
-    __syncthreads();
-    float2 t = make_float2(red[0], red[1]);
-#pragma unroll
-    for (int w = 1; w < SYNC_WAVES; ++w) { t.x += red[2 * w]; t.y += red[2 * w + 1]; }
-    return t;
-}
-__device__ __forceinline__ int block_max_i(int v, int *red) {
-    v = wave_max_i(v);
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-    __syncthreads();
-    int t = red[0];
-#pragma unroll
-    for (int w = 1; w < SYNC_WAVES; ++w) t = max(t, red[w]);
-    return t;
-}
+// block-wide exchange over the SYNC_WAVES waves, the wave partials combined in wave order
 // (min of a, max of b) over the waves in one exchange (scratch: 2 SYNC_WAVES slots).  LEAD: the barrier
 // that keeps the slots from being overwritten while an earlier exchange still reads them; the item
 // loop's slots were last read before the previous item's closing barrier, so it passes false.
@@ -384,16 +352,6 @@ __device__ __forceinline__ int2 block_minmax_i(int a, int b, int *red) {
     int2 t = make_int2(red[0], red[1]);
 #pragma unroll
     for (int w = 1; w < SYNC_WAVES; ++w) { t.x = min(t.x, red[2 * w]); t.y = max(t.y, red[2 * w + 1]); }
-    return t;
-}
-__device__ __forceinline__ int block_min_i(int v, int *red) {
-    v = wave_min_i(v);
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-    __syncthreads();
-    int t = red[0];
-#pragma unroll
-    for (int w = 1; w < SYNC_WAVES; ++w) t = min(t, red[w]);
     return t;
 }
 
