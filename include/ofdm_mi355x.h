@@ -138,7 +138,10 @@ int ofdm_rx_frames_dump(ofdm_ctx *ctx, const ofdm_cfg *cfg, const void *d_tx, co
                         uint64_t first_frame, int64_t n_frames, const double *snr_db, int n_snr,
                         void *d_counters, void *d_eq, void *d_dbits);
 /* Whole sweep ("main()" SNR loop, OFDM.c:1187-1222): Tx + Rx in device-resident chunks of at most
- * chunk_frames frames; writes host counters [n_snr][OFDM_NCOUNTERS]. */
+ * chunk_frames frames (0: 2^22, and at least 4 chunks when n_frames >= 2^20); writes host counters
+ * [n_snr][OFDM_NCOUNTERS].  With more than one chunk the Tx of chunk k+1 runs on a second stream owned
+ * by the context, ordered by events against the context's stream (double-buffered Tx batches); the
+ * counters do not depend on the chunking. */
 int ofdm_symbol_sweep(ofdm_ctx *ctx, const ofdm_cfg *cfg, const double *snr_db, int n_snr,
                       uint64_t first_frame, int64_t n_frames, int64_t chunk_frames,
                       int64_t *counters);
