@@ -74,7 +74,8 @@ struct FrameArgs {
     unsigned long long *stamps;     // OFDM_FRAME_STAMPS builds: cycles per receiver phase [8]
     // sync -> symbol hand-off (one chunk of items; item g = trial (g / n_snr), SNR (g % n_snr))
     int64_t item0, n_items;         // first global item of the chunk, items in it
-    float2 *win;                    // [n_items][2 + n_data][64]: LTF1, LTF2, data windows after CFO
+    float2 *win;                    // hand-off tiles (win_at): LTF1, LTF2, data windows after CFO
+    int32_t ipb;                    // items per frame_sym_kernel block = items per hand-off tile
     int4 *info;                     // [n_items]: packet_idx, sync_fail, oob, rx_start
     int32_t add_totals;             // 1 on the last chunk: add frames / symbols / bits / terms
 };
@@ -295,6 +296,15 @@ __device__ __forceinline__ float2 cfo_rot(float2 v, double f_ts, int i) {
     s = __builtin_amdgcn_sinf(fr);
     c = __builtin_amdgcn_cosf(fr);
     return make_float2(v.x * c - v.y * s, v.x * s + v.y * c);
+}
+
+// Hand-off layout: tiles of ipb items (one frame_sym_kernel block), each tile [64 samples][ipb items][nw
+// windows] float2, so that a symbol-kernel wave reading sample n of its lanes' windows reads one
+// contiguous row segment (its 16 items x 4 windows = 512 B for the reference frame), where an item-major
+// layout made every lane's 8-byte load a different cache line.
+__host__ __device__ inline float2 *win_item(float2 *win, int ipb, int nw, int64_t item) {
+    const int64_t tile = item / ipb, it = item - tile * ipb;
+    return win + tile * 64 * (int64_t)(ipb * nw) + it * nw;      // sample n of window w at [n * ipb * nw + w]
 }
 
 // j-th frame sample the receiver reads (j < 160 + 64 nd): the coarse-CFO lag window [80, 112)
@@ -786,14 +796,19 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
         // off directly: LTF1 [192,256), LTF2 [256,320), data d [336 + 80 d, +64) (OFDM.c:830-850,
         // 1024-1040) ----
         const int nw = 2 + a.n_data;
-        float2 *dst = a.win + i * (int64_t)(nw * 64);
+        float2 *dst = win_item(a.win, a.ipb, nw, i);
+        const int row = a.ipb * nw;                            // float2 between samples n and n + 1
 #ifndef OFDM_FRAME_CFO_TWO_STEP
         const double fcf_ts = (fc + ff) * TS;
 #endif
-        // hand-off sample j = window j / 64, sample j % 64 (contiguous stores); the dump rotates all nfr
+        // hand-off element j = sample j / nw of window j % nw: consecutive lanes fill the item's nw
+        // adjacent slots of a tile row (j / nw by a 16-bit reciprocal, exact for j < 64 nw <= 640);
+        // the dump rotates all nfr samples
         const int nrot = dbg ? nfr : 64 * nw;
+        const uint32_t inv_nw = (65536u + (uint32_t)nw - 1u) / (uint32_t)nw;
         for (int j = tid; j < nrot; j += SYNC_THREADS) {
-            int k = needed_k(j + 32), w = j >> 6, n = j & 63;
+            int n = (int)(((uint32_t)j * inv_nw) >> 16), w = j - n * nw;
+            int k = needed_k(64 * w + n + 32);
             if (dbg) {
                 k = j; w = -1;
                 if (k >= 192 && k < 320) {
@@ -809,7 +824,7 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
             const float2 v = cfo_rot(fr[k], fcf_ts, k);
 #endif
             if (dbg) a.dbg_frame[k] = v;
-            if (w >= 0) dst[w * 64 + n] = v;
+            if (w >= 0) dst[n * row + w] = v;
         }
         FR_STAMP(4);                                           // coarse + fine CFO + hand-off
         if (tid == 0) {
@@ -869,7 +884,8 @@ __global__ __launch_bounds__(SYM_THREADS, FRAME_SYM_MINB) void frame_sym_kernel(
         const int64_t i = base + item_l;
         const bool item_ok = item_l < ipb && i < a.n_items;
         const bool dlane = item_ok && role >= 2 && dsym < a.n_data;
-        const float2 *src = a.win + (item_ok ? i : 0) * (int64_t)(nw * 64) + w * 64;
+        const float2 *src = win_item(a.win, ipb, nw, item_ok ? i : base) + w;
+        const int row = ipb * nw;                                  // float2 between samples n and n + 1
         float2 x[64];
         // load fused with the first radix-4 stage, 16 samples at a time (fft() = DFT(x (-1)^n))
         static_for<0, 4>([&](auto gc) {
@@ -878,7 +894,7 @@ __global__ __launch_bounds__(SYM_THREADS, FRAME_SYM_MINB) void frame_sym_kernel(
             opaque(sp);
             static_for<0, 16>([&](auto pc) {
                 constexpr int n = 16 * (decltype(pc)::value >> 2) + 4 * g + (decltype(pc)::value & 3);
-                const float2 v = gld(sp, n);
+                const float2 v = gld(sp, n * row);
                 x[n] = (n & 1) ? make_float2(-v.x, -v.y) : v;
             });
             static_for<0, 4>([&](auto ic) { dif_stage1<false, 4 * g + decltype(ic)::value>(x); });
@@ -1058,7 +1074,8 @@ constexpr int64_t FRAME_CHUNK_ITEMS = int64_t(1) << 18;   // items per sync -> s
 // K4b then K4b' over a.n_items items starting at a.item0, through the context's hand-off buffer
 static int run_frame_chunk(Ctx *c, FrameArgs &a) {
     const int nw = 2 + a.n_data;
-    const size_t wbytes = (size_t)a.n_items * nw * 64 * sizeof(float2);
+    a.ipb = (SYM_THREADS / 4) / ((a.n_data + 1) / 2);
+    const size_t wbytes = (size_t)((a.n_items + a.ipb - 1) / a.ipb) * a.ipb * nw * 64 * sizeof(float2);
     int rc = c->ensure(&c->d_scratch, &c->cap_scratch, wbytes + (size_t)a.n_items * sizeof(int4) + 256);
     if (rc) return rc;
     a.win = (float2 *)c->d_scratch;
