@@ -2,6 +2,4 @@ set -u
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_gpu_frame.py tests/test_gpu_message.py tests/test_gpu_dist.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/frame_tests.log 2>&1; rc=$?; echo "frame tests rc=$rc"; tail -3 gpurun_out/frame_tests.log
 [ $rc -ge 2 ] && exit $rc
-SYMBOLS=1000000 VARIANTS="default default" WORKLOADS="frame" bash tools/ab.sh
-timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_fr -o run --output-format csv -- python3 bench.py --workload frame --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/prof_fr.log 2>&1; echo "prof rc=$?"
-cat gpurun_out/prof_fr/run_kernel_stats.csv 2>/dev/null | head -4
+SYMBOLS=1000000 VARIANTS="default inter default inter" WORKLOADS="frame" bash tools/ab.sh
