@@ -4,7 +4,9 @@
 // sweeps (c2/c3/c4, the benchmark) run the packed receivers of ofdm_rxpack.hip instead (launch_rx);
 // the kernels here serve complex noise, the 4-tap Rayleigh channel (c5) and noiseless runs.
 //
-// Mapping: ONE LANE OWNS ONE 64-SAMPLE WINDOW (a data symbol or the LTF pair); its 64-point FFT
+// K1 (the standalone fft()/ifft()) runs one transform per lane quad (fft64_quad_kernel); the Tx and
+// receiver kernels below keep the register mapping:
+// ONE LANE OWNS ONE 64-SAMPLE WINDOW (a data symbol or the LTF pair); its 64-point FFT
 // lives in that lane's VGPRs (ofdm_device.h).  In LS mode a wave carries 21 frames as lanes
 // {E, D0, D1}: the data lanes fetch S = F1 + F2 (OFDM.c:830-850) from their E lane with ds_bpermute.
 //
@@ -230,7 +232,11 @@ __global__ __launch_bounds__(256) void fft64_quad_kernel(const float2 *__restric
         const float4 *src = reinterpret_cast<const float4 *>(in + (t < n ? t : 0) * 64 + 16 * q);
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
+#ifdef OFDM_K1_ABL_LOAD   // ablation (wrong results): each quad's loads contiguous 64 B per instruction
+            const float4 v = t < n ? src[4 * c - 7 * q] : make_float4(0.f, 0.f, 0.f, 0.f);
+#else
             const float4 v = t < n ? src[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+#endif
             x[u][2 * c] = make_float2(v.x, v.y);
             x[u][2 * c + 1] = make_float2(v.z, v.w);
         }
@@ -257,7 +263,11 @@ __global__ __launch_bounds__(256) void fft64_quad_kernel(const float2 *__restric
             static_for<0, 16>([&](auto pc) {
                 constexpr int pos = decltype(pc)::value;
                 constexpr int kp = ((pos & 3) << 2) | (pos >> 2);   // rev16 is its own inverse
+#ifdef OFDM_K1_ABL_STORE  // ablation (wrong results): every store instruction writes 512 contiguous bytes
+                out[(t0 - (threadIdx.x >> 2) + 16 * (threadIdx.x >> 6)) * 64 + 64 * pos + (threadIdx.x & 63)] = cscale(x[u][pos], out_scale);
+#else
                 dst[4 * kp] = cscale(x[u][pos], out_scale);
+#endif
             });
         }
     }
