@@ -133,3 +133,32 @@ def test_frame_sweep_word_stats(engine, oracle, pkg):
         assert c[q, abi.C_WL_MAX_Q] / 2 ** 20 == pytest.approx(hi, abs=1e-5)
         ma = max(abs(lo), abs(hi))
         assert c[q, abi.C_WL_BITS] == (1 if ma < 1 else int(np.ceil(np.log2(ma))) + 1)
+
+
+@pytest.mark.parametrize("msg", [b"Twelve chars", b"x" * 20 + b" three syms", bytes(range(32, 127)) + b"!"],
+                         ids=["1-symbol", "3-symbol", "8-symbol"])
+def test_frame_sweep_vs_oracle_lengths(msg_engine, oracle, pkg, msg):
+    """Frame lengths at the edges of the symbol kernel's tiling and the sync kernel's LDS budget: 1 data
+    symbol (one quad per trial, an idle data lane), 3 (two quads, the second half empty) and 8 (the
+    longest capture, 5955 samples: detection chunks of 47 positions, two crossing words per lane)."""
+    from ofdm_amd import abi
+    nd = msg_engine.set_message(msg)
+    assert nd == -(-8 * len(msg) // 96)
+    oracle.set_message(msg)
+    try:
+        w = msg_engine.transmitter("c", "message")
+        L = abi.capture_len(nd)
+        o = msg_engine.receiver(w[333:333 + L], "c", "message")
+        assert not o["sync_fail"] and o["message"].rstrip(" ") == msg.decode()
+        cfg = pkg.make_cfg(payload="message")
+        snrs = [8.0, 14.0]
+        n = 160
+        g, gp = msg_engine.frame_sweep(cfg, snrs, n, want_packet_idx=True)
+        r, rp = oracle.frame_sweep(oracle.cfg(payload="message"), snrs, 0, n, "c", dump_pidx=True)
+        assert np.mean(gp == rp) > 0.99
+        for k in (0, 1, 2, 6):                                         # frames, symbols, bits, evm terms
+            assert np.array_equal(g[:, k], r[:, k])
+        assert g[0, 1] == nd * n and g[0, 2] == 96 * nd * n
+        assert np.all(np.abs(g[:, 3] - r[:, 3]) <= 96 * nd * np.sum(gp != rp, axis=1) + 3)
+    finally:
+        oracle.set_message(b"Hey! I am Vivaswan")
