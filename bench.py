@@ -70,9 +70,21 @@ def load_pmc(workload: str) -> dict:
     tools/pmc_summary.py from tools/gpu_profile.sh runs), or {}."""
     p = ROOT / "profiles" / "pmc_summary.json"
     try:
-        return json.loads(p.read_text()).get(workload, {})
+        # c4 launches c3's receiver on c3's configuration (only the chunking differs): c3's counters apply
+        return json.loads(p.read_text()).get({"c4": "c3"}.get(workload, workload), {})
     except Exception:
         return {}
+
+
+def issue_cap(pmc: dict, frac: float) -> dict:
+    """The instruction-mix cap of the kernel's loop (tools/isa_mix.py --record: class-priced issue cycles of
+    its gfx950 assembly) and this run's fraction of it, when recorded."""
+    m = pmc.get("issue_model")
+    if not m:
+        return {}
+    return {"issue_model_cap_frac": m["cap_frac"], "frac_of_issue_model_cap": frac / m["cap_frac"],
+            "issue_model_note": "cap = 2 x loop VALU / class-priced SIMD cycles at %d waves/SIMD (modelled)"
+                                % m["waves_per_simd"]}
 
 
 def cpu_model() -> str:
@@ -369,7 +381,8 @@ def main():
                           "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC)",
                           "instr_per_unit": ipu, "kernel": kernel, "avg_launch_ms": rx_avg_s * 1e3,
                           "launches": rx_n, "units_per_launch": units_per_launch,
-                          "pmc_source": "profiles/pmc_summary.json[%s]" % args.workload}
+                          "pmc_source": "profiles/pmc_summary.json[%s]" % {"c4": "c3"}.get(args.workload, args.workload),
+                          **issue_cap(pmc, units_per_launch * ipu / rx_avg_s / VALU_PEAK_PER_S)}
                          if ipu else
                          {"bound": "valu", "achieved": None, "peak": VALU_PEAK_PER_S, "unit": "wave-instr/s",
                           "frac": None, "traffic": traffic, "kernel": kernel, "avg_launch_ms": rx_avg_s * 1e3,

@@ -13,14 +13,19 @@ wave64 instruction at 2 / 4 waves per SIMD):
 The loop is the largest basic block between a label and its backward branch (or --loop N: the N-th
 largest)."""
 import collections
+import json
 import re
 import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
 
 FAST_OPS = re.compile(r"^v_(add|sub|subrev|mul|fma|fmac|fmamk|fmaak)_f32|^v_(add|sub|subrev)_u32|^v_(and|or|xor)_b32"
                       r"|^v_bitop3_b32|^v_mov_b32|^v_add_co_u32|^v_sub_co_u32")
 TRANS = re.compile(r"^v_(log|sin|cos|sqrt|rcp|exp|rsq)_f32")
 COST = {2: {"fast": 2.35, "slow": 4.30, "trans": 8.23, "cnd": 16.2},
         4: {"fast": 1.97, "slow": 3.15, "trans": 6.12, "cnd": 12.5}}
+COST[3] = {k: 0.5 * (COST[2][k] + COST[4][k]) for k in COST[2]}     # interpolated (not measured)
 
 
 def classify(op, args):
@@ -76,11 +81,24 @@ def main(argv):
             ops[(c, op)] += 1
     valu = sum(cls[k] for k in ("fast", "slow", "trans", "cnd"))
     print(f"loop lines {a}-{b}: VALU {valu}  " + "  ".join(f"{k} {v}" for k, v in sorted(cls.items())))
-    for w in (2, 4):
+    priced = {}
+    for w in (2, 3, 4):
         cyc = sum(COST[w][k] * cls[k] for k in COST[w])
-        print(f"  priced issue cycles at {w} waves/SIMD: {cyc:.0f}")
+        priced[w] = cyc
+        # the nominal issue peak is one wave-instruction per 2 SIMD cycles: this mix can reach 2 VALU / cyc of it
+        print(f"  priced issue cycles at {w} waves/SIMD: {cyc:.0f}  (mix cap: {2 * valu / cyc:.3f} of the nominal peak)")
     for (c, op), n in ops.most_common(40):
         print(f"  {c:6s} {op:28s} {n}")
+    if "--record" in argv:       # --record WORKLOAD --waves W: store the cap beside the workload's PMC summary
+        wl = argv[argv.index("--record") + 1]
+        w = int(argv[argv.index("--waves") + 1]) if "--waves" in argv else 2
+        out = ROOT / "profiles" / "pmc_summary.json"
+        summary = json.loads(out.read_text())
+        summary[wl]["issue_model"] = {
+            "kernel": name, "loop_valu": valu, "classes": dict(cls), "waves_per_simd": w,
+            "priced_cycles": priced[w], "cap_frac": 2 * valu / priced[w],
+            "source": "tools/isa_mix.py on the gfx950 assembly; class costs profiles/r01/ubench/"}
+        out.write_text(json.dumps(summary, indent=1, sort_keys=True))
 
 
 if __name__ == "__main__":
