@@ -98,6 +98,8 @@ def main(argv):
         "trace": trace,
         "note": "FETCH_SIZE doubled (gfx950 reports half of wide streaming reads); sums over dispatches / units",
     }
+    if "issue_model" in summary.get(workload, {}):          # tools/isa_mix.py --record: a static-code figure
+        entry["issue_model"] = summary[workload]["issue_model"]
     summary[workload] = entry
     out.write_text(json.dumps(summary, indent=1, sort_keys=True))
     print(json.dumps(entry, indent=1))
