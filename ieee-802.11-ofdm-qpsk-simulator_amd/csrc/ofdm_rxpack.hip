@@ -176,7 +176,22 @@ __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_
 #define PKEYS a.k0, a.k1
 #endif
     const int64_t n_groups = (a.n_frames + PK_FRAMES - 1) / PK_FRAMES;
-    for (int64_t grp = blockIdx.x; grp < n_groups; grp += gridDim.x) {
+    // Work items: the groups of the full rounds (every block takes gridDim.x-strided groups, all SNR points),
+    // then the T tail groups with their SNR points split S ways over up to S T <= gridDim.x blocks, so the
+    // last round is not T groups long on T blocks while the rest of the grid idles.  The counters are
+    // integer sums: the split does not change them.
+    const int64_t B = gridDim.x, R = n_groups / B, T = n_groups - R * B;
+#ifndef OFDM_PACK_NO_TAIL_SPLIT
+    const int S = T > 0 ? (int)max<int64_t>(1, min<int64_t>(4, B / T)) : 1;
+#else
+    const int S = 1;
+#endif
+    const int64_t n_items = R * B + T * S;
+    for (int64_t w = blockIdx.x; w < n_items; w += B) {
+        const bool tail = w >= R * B;
+        const uint32_t tw = tail ? (uint32_t)(w - R * B) : 0u;      // < T S <= gridDim.x
+        const int64_t grp = tail ? R * B + (int64_t)(tw / (uint32_t)S) : w;
+        const int sub = tail ? (int)(tw % (uint32_t)S) : 0, ns = tail ? S : 1;
         __syncthreads();                                   // every wave is done with the last group
         // group-invariant addresses are re-derived from the thread index here, not held across the SNR
         // loop (they would be the only values spilled)
@@ -214,7 +229,7 @@ __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_
         const int64_t fl = grp * PK_FRAMES + lane;
         const bool valid = fl < a.n_frames;
         const uint64_t f = a.first_frame + (uint64_t)fl;
-        for (int q = wv; q < a.n_snr; q += 4) {
+        for (int q = wv + 4 * sub; q < a.n_snr; q += 4 * ns) {
             uint32_t flo = (uint32_t)f, fhi = (uint32_t)(f >> 32);
             opaque(flo); opaque(fhi);
             const float sigma = a.sigma[q];
