@@ -195,7 +195,7 @@ int ofdm_ctx_destroy(ofdm_ctx *ctx) {
     for (auto ev : c->pool) hipEventDestroy(ev);
     if (c->tx_stream) hipStreamSynchronize(c->tx_stream);
     for (void *p : {(void *)c->d_ltf[0], (void *)c->d_ltf[1], (void *)c->d_ltf2_rows[0], (void *)c->d_ltf2_rows[1], c->d_tx, c->d_bits, c->d_cnt, c->d_scratch,
-                    c->d_scratch2, c->d_wave, c->d_tx2, c->d_bits2})
+                    c->d_scratch2, c->d_wave, c->d_tx2, c->d_bits2, c->d_work})
         if (p) hipFree(p);
     for (hipEvent_t ev : {c->ev_start, c->ev_tx[0], c->ev_tx[1], c->ev_rx[0], c->ev_rx[1]})
         if (ev) hipEventDestroy(ev);
@@ -357,6 +357,9 @@ static int rx_common(Ctx *c, const ofdm_cfg *cfg, const void *d_tx, const void *
         HIPOK(hipMalloc(&a.stamps, 64));
         HIPOK(hipMemset(a.stamps, 0, 64));
 #endif
+        if (!c->d_work) HIPOK(hipMalloc(&c->d_work, 256));
+        a.work = (unsigned long long *)c->d_work;
+        HIPOK(hipMemsetAsync(c->d_work, 0, sizeof(unsigned long long), c->stream));
         c->tic(Ctx::K_RX);
         launch_rx(c->stream, a, *cfg, dump, grid);
         c->toc();

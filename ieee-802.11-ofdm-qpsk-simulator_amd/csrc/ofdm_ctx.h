@@ -34,6 +34,7 @@ struct Ctx {
     hipStream_t tx_stream = nullptr;
     hipEvent_t ev_start = nullptr, ev_tx[2] = {nullptr, nullptr}, ev_rx[2] = {nullptr, nullptr};
     void *d_wave = nullptr;
+    void *d_work = nullptr;          // K3c's work-item counter (one receiver launch in flight per context)
     size_t cap_tx = 0, cap_bits = 0, cap_cnt = 0, cap_scratch = 0, cap_scratch2 = 0, cap_wave = 0;
     // frame-mode waveform cache (per conv/payload/message)
     int wave_key = -1;

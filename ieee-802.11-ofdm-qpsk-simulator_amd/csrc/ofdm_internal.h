@@ -55,6 +55,7 @@ struct RxArgs {
     uint32_t *dump_bits;
     int64_t dump_frames;               // leading dimension of the dumps (frames)
     unsigned long long *stamps;        // OFDM_RX_STAMPS builds: cycles per receiver phase [5]
+    unsigned long long *work;          // K3c: work items handed out past the first gridDim.x (zeroed per launch)
     float sigma[OFDM_MAX_SNR];
 };
 

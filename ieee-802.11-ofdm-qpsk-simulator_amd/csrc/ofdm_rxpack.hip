@@ -180,18 +180,24 @@ __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_
     // then the T tail groups with their SNR points split S ways over up to S T <= gridDim.x blocks, so the
     // last round is not T groups long on T blocks while the rest of the grid idles.  The counters are
     // integer sums: the split does not change them.
-    const int64_t B = gridDim.x, R = n_groups / B, T = n_groups - R * B;
+    // (32-bit item arithmetic: a launch holds at most 2^23 frames = 2^17 groups)
+    const int B = (int)gridDim.x, G = (int)n_groups, R = G / B, T = G - R * B;
 #ifndef OFDM_PACK_NO_TAIL_SPLIT
-    const int S = T > 0 ? (int)max<int64_t>(1, min<int64_t>(4, B / T)) : 1;
+    const int S = T > 0 ? max(1, min(4, B / T)) : 1;
 #else
     const int S = 1;
 #endif
-    const int64_t n_items = R * B + T * S;
-    for (int64_t w = blockIdx.x; w < n_items; w += B) {
+    const int n_items = R * B + T * S;
+    // Items past the first gridDim.x are handed out one at a time from a.work: during an item's prologue
+    // thread 128 fetches the block's next item and wave 2 warms L2 with that item's Tx rows.  Blocks that
+    // finish early take more, so the launch ends when the work does, not when the slowest block's static
+    // share does.  The next item waits in LDS (read after the SNR loop: nothing 64-bit is held across it).
+    __shared__ int next_item;
+    for (int w = blockIdx.x; w < n_items; w = __builtin_amdgcn_readfirstlane(next_item)) {
         const bool tail = w >= R * B;
-        const uint32_t tw = tail ? (uint32_t)(w - R * B) : 0u;      // < T S <= gridDim.x
-        const int64_t grp = tail ? R * B + (int64_t)(tw / (uint32_t)S) : w;
-        const int sub = tail ? (int)(tw % (uint32_t)S) : 0, ns = tail ? S : 1;
+        const int tw = tail ? w - R * B : 0;                           // < T S <= gridDim.x
+        const int64_t grp = tail ? R * B + tw / S : w;
+        const int sub = tail ? tw % S : 0, ns = tail ? S : 1;
         __syncthreads();                                   // every wave is done with the last group
         // group-invariant addresses are re-derived from the thread index here, not held across the SNR
         // loop (they would be the only values spilled)
@@ -203,27 +209,36 @@ __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_
         if (t < PK_SYMS) {
 #endif
             clean_spectrum(a, grp * PK_SYMS + t, &spec[0][t & 1][t >> 1]);
-        } else if (t < PK_SYMS) {
         } else {
             const int j = t - PK_SYMS;
             const uint32_t *src = a.bits + 7 * a.pitch + grp * PK_SYMS + j;
             truth[0][j] = src[0];
             truth[1][j] = src[a.pitch];
             truth[2][j] = src[2 * a.pitch];
-#ifndef OFDM_PACK_NO_L2_WARM
-            // warm L2 with this block's next group (64 rows x 1 KB: one 4-byte LDS-DMA read per 128-B line,
-            // into a dummy LDS word), so the next prologue's loads hit L2 instead of HBM
-            const int64_t ng = grp + gridDim.x;
-            if (ng < n_groups) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int line = j + PK_SYMS * i;                       // 0..511
-                    const float2 *p = a.tx + (int64_t)(16 + (line >> 3)) * a.pitch + ng * PK_SYMS + (line & 7) * 16;
-                    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)p,
-                                                     (__attribute__((address_space(3))) void *)pf_dummy, 4, 0, 0);
-                }
-            }
+            if (j < 64) {                                  // wave 2: the next item
+#ifndef OFDM_PACK_STATIC_ITEMS
+                int nx = 0;
+                if (j == 0) nx = B + (int)atomicAdd(a.work, 1ull);
+                nx = __builtin_amdgcn_readfirstlane(__shfl(nx, 0, 64));
+#else
+                const int nx = w + B;
 #endif
+                if (j == 0) next_item = nx;
+#ifndef OFDM_PACK_NO_L2_WARM
+                // warm L2 with the next item's group (64 rows x 1 KB: one 4-byte LDS-DMA read per 128-B
+                // line, into a dummy LDS word), so the next prologue's loads hit L2 instead of HBM
+                if (nx < n_items) {
+                    const int64_t ng = nx < R * B ? nx : R * B + (nx - R * B) / S;
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const int line = j + 64 * i;                       // 0..511
+                        const float2 *p = a.tx + (int64_t)(16 + (line >> 3)) * a.pitch + ng * PK_SYMS + (line & 7) * 16;
+                        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)p,
+                                                         (__attribute__((address_space(3))) void *)pf_dummy, 4, 0, 0);
+                    }
+                }
+#endif
+            }
         }
         __syncthreads();
         const int64_t fl = grp * PK_FRAMES + lane;
