@@ -716,23 +716,41 @@ __global__ __launch_bounds__(256, OFDM_RX_LS_WAVES) void rx_ls_kernel(RxArgs a) 
     const int64_t n_groups = (a.n_frames + LS_GROUP_FRAMES - 1) / LS_GROUP_FRAMES;
     [[maybe_unused]] const int64_t P = a.pitch;
 
+    // Groups past the first gridDim.x are handed out from a per-launch atomic counter (a.work), one group
+    // ahead of the staging: the block always knows the group it stages next (nxt) and thread 0 fetches
+    // the one after it into LDS during the current group; blocks that run fast take more groups.  The LDS
+    // slot alternates with the group's parity: a slot is rewritten only after a barrier that follows
+    // every read of it.
+    __shared__ int next_group[2];
+    int par = 0;
     int cur = 0;
     int64_t grp = blockIdx.x;
     if (grp < n_groups) {
         stage_group<G>(a, grp * LS_GROUP_SYMS, sbuf[0], a.ltf2_rows, wv, lane);
         stage_truth(a, grp * LS_GROUP_SYMS, &struth[0][0][0], wv, lane, LS_GROUP_SYMS);
     }
+#ifndef OFDM_RX_STATIC_GROUPS
+    if (threadIdx.x == 0) next_group[1] = (int)gridDim.x + (int)atomicAdd(a.work, 1ull);
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+#ifndef OFDM_RX_STATIC_GROUPS
+    int64_t nxt = __builtin_amdgcn_readfirstlane(next_group[1]);
+#else
+    int64_t nxt = grp + gridDim.x;
+#endif
     RxStamp sp;
     sp.start();
-    for (; grp < n_groups; grp += gridDim.x) {
+    for (; grp < n_groups;) {
         const int64_t fl = grp * LS_GROUP_FRAMES + fr;
         const bool valid = fr < LS_GROUP_FRAMES && fl < a.n_frames;
         const uint64_t f = a.first_frame + (uint64_t)fl;
         const uint32_t f_lo = (uint32_t)f, f_hi = (uint32_t)(f >> 32);
         float2 h[4] = {make_float2(1.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f)};
-        const int64_t nxt = grp + gridDim.x;
+#ifndef OFDM_RX_STATIC_GROUPS
+        // the group after nxt (read after this group's closing barrier; the previous value was read before it)
+        if (threadIdx.x == 0) next_group[par] = (int)gridDim.x + (int)atomicAdd(a.work, 1ull);
+#endif
         if constexpr (FADE) {
             // lane = staged column: 0..41 the data symbols (in place), 42..62 frame lane - 42's 2T (x) h
             const bool dcol = lane < LS_GROUP_SYMS;
@@ -786,6 +804,13 @@ __global__ __launch_bounds__(256, OFDM_RX_LS_WAVES) void rx_ls_kernel(RxArgs a) 
         __syncthreads();                                   // and every wave is done with this one
         sp.mark(4);
         cur ^= 1;
+        grp = nxt;
+#ifndef OFDM_RX_STATIC_GROUPS
+        nxt = __builtin_amdgcn_readfirstlane(next_group[par]);
+#else
+        nxt = grp + gridDim.x;
+#endif
+        par ^= 1;
     }
     sp.flush(a.stamps);
     block_flush(a, sacc);
