@@ -78,6 +78,7 @@ struct FrameArgs {
     int32_t ipb;                    // items per frame_sym_kernel block = items per hand-off tile
     int4 *info;                     // [n_items]: packet_idx, sync_fail, oob, rx_start
     int32_t add_totals;             // 1 on the last chunk: add frames / symbols / bits / terms
+    unsigned long long *work;       // sync kernel: items handed out past the first gridDim.x (zeroed per launch)
 };
 
 #ifdef OFDM_FRAME_STAMPS   // diagnostic build: s_memtime per phase, summed over the grid
@@ -325,7 +326,10 @@ constexpr int SYNC_THREADS = FRAME_SYNC_THREADS;   // the waves that share each 
 constexpr int SYNC_WAVES = SYNC_THREADS / 64;
 static_assert(SYNC_WAVES >= 2 && SYNC_WAVES <= 4, "block reductions use 2..4 waves");
 // per-item scratch words after the accumulators: floats [0, 8) (block float sums), ints [8, 32)
-constexpr int RED_WORDS = 32, RED_I_MAX = 0, RED_I_PREFIX = 4, RED_I_MINMAX = 8;
+constexpr int RED_WORDS = 32, RED_I_MAX = 0, RED_I_PREFIX = 4, RED_I_MINMAX = 8, RED_I_NEXT = 20;
+#ifndef FRAME_ITEM_RUN
+#define FRAME_ITEM_RUN 4            // items per hand-out of the sync kernel's work counter
+#endif
 constexpr int ACC_SLOTS = 12;       // per-SNR block accumulators: 9 counter sums + word-length min / max
 __host__ __device__ inline int cross_words(int cap_len) { return (cap_len - 47 + 63) / 64 + 1; }
 // capture region: cap_len + 8 samples, the capture starting at sample (rx_start & 3) so that every
@@ -391,7 +395,17 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
     unsigned long long stamp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long stamp_t = __builtin_amdgcn_s_memtime();
 #endif
-    for (int64_t i = blockIdx.x; i < a.n_items; i += gridDim.x) {
+    // Items go out in runs of FRAME_ITEM_RUN: block b starts with run b, the runs past the first gridDim.x
+    // come from a per-launch atomic counter, so blocks that run fast take more runs.  Thread 0 fetches the
+    // next run at the first item of the current one (its wait on the atomic is paid once per run), every
+    // thread reads it after the capture barrier of the run's last item.  One atomic per item serialises on
+    // the counter's address at ~10 M/s, below the kernel's item rate.
+#ifndef OFDM_FRAME_STATIC_ITEMS
+    int64_t run_end = (int64_t)blockIdx.x * FRAME_ITEM_RUN + FRAME_ITEM_RUN;
+    for (int64_t i = run_end - FRAME_ITEM_RUN, inext = 0; i < a.n_items; i = inext) {
+#else
+    for (int64_t i = blockIdx.x, inext = 0; i < a.n_items; i = inext) {
+#endif
 #ifndef FRAME_HOIST_LANE
         // lane-derived values (addresses, sample indices, fp64 instants) are re-derived per item instead of
         // being hoisted out of the item loop and held in ~40 VGPRs across every phase
@@ -407,6 +421,10 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
         KArgs *ap = (KArgs *)__builtin_amdgcn_kernarg_segment_ptr();
         asm volatile("" : "+s"(ap));
         KArgs &a = *ap;
+#endif
+#ifndef OFDM_FRAME_STATIC_ITEMS
+        if (threadIdx.x == 0 && i == run_end - FRAME_ITEM_RUN)
+            redi[RED_I_NEXT] = (int)gridDim.x + (int)atomicAdd(a.work, 1ull);
 #endif
         const int64_t g = a.item0 + i;
         int q;
@@ -499,6 +517,16 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
         }
         for (int k = tid; k < cross_words(L); k += SYNC_THREADS) cross[k] = 0ull;
         __syncthreads();
+#ifndef OFDM_FRAME_STATIC_ITEMS
+        if (i + 1 < run_end) {
+            inext = i + 1;
+        } else {
+            inext = (int64_t)__builtin_amdgcn_readfirstlane(redi[RED_I_NEXT]) * FRAME_ITEM_RUN;
+            run_end = inext + FRAME_ITEM_RUN;
+        }
+#else
+        inext = i + gridDim.x;
+#endif
         FR_STAMP(0);                                           // capture + noise
 
         // ---- Word_Optimization_Analysis(Rx_filter_signal) (OFDM.c:38-73, 962-967): the full RRC
@@ -1062,11 +1090,11 @@ static int32_t word_bits(double mn, double mx) {
     return max_abs < 1.0f ? 1 : (int32_t)std::ceil(std::log2((double)max_abs)) + 1;
 }
 
-static unsigned occupancy_grid(const void *kernel, int threads, size_t lds, int cus, int64_t blocks) {
+static unsigned occupancy_grid(const void *kernel, int threads, size_t lds, int cus, int64_t blocks, int waves = 2) {
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, lds) != hipSuccess || per_cu < 1)
         per_cu = 2;
-    return (unsigned)std::max<int64_t>(1, std::min<int64_t>(blocks, (int64_t)per_cu * cus * 2));
+    return (unsigned)std::max<int64_t>(1, std::min<int64_t>(blocks, (int64_t)per_cu * cus * waves));
 }
 
 constexpr int64_t FRAME_CHUNK_ITEMS = int64_t(1) << 18;   // items per sync -> symbol hand-off (<= 1 GB)
@@ -1086,9 +1114,16 @@ static int run_frame_chunk(Ctx *c, FrameArgs &a) {
 #else
     a.fr_in_cap = fr_in_capture(a.cap_len, a.n_data);
 #endif
+    if (!c->d_work) HIPOK(hipMalloc(&c->d_work, 256));
+    a.work = (unsigned long long *)c->d_work;
+    HIPOK(hipMemsetAsync(c->d_work, 0, sizeof(unsigned long long), c->stream));
+#ifndef OFDM_FRAME_SYNC_WAVES
+#define OFDM_FRAME_SYNC_WAVES 2
+#endif
+    const int sync_waves = OFDM_FRAME_SYNC_WAVES;
     hipLaunchKernelGGL(frame_sync_kernel,
                        dim3(occupancy_grid(reinterpret_cast<const void *>(&frame_sync_kernel), SYNC_THREADS, lds,
-                                           c->cus, a.n_items)),
+                                           c->cus, a.n_items, sync_waves)),
                        dim3(SYNC_THREADS), lds, c->stream, a);
     const int ipb = (SYM_THREADS / 4) / ((a.n_data + 1) / 2);
     const bool dump = a.dbg_eq || a.dbg_bits || a.dbg_res;
