@@ -12,8 +12,9 @@ Workloads (BASELINE.json configs; --workload):
      GPU (weak scaling: the largest single-GPU config; the driver's 1/2/4/8-GPU curve runs this)
   c2 (configs[1])          ideal CSI, 1e6 symbols/point, 1 GPU
   c4 (configs[3])          c3's chain, 1e8 symbols/point in TOTAL, split over the ranks (strong)
-  c5 (configs[4])          4-tap Rayleigh + ZF (LS), complex AWGN, 1e9 symbol-SNR evaluations in
-                           TOTAL (6.25e7 symbols/point x 16 points), split over the ranks (strong)
+  c5 (configs[4])          4-tap Rayleigh + ZF (LS), real AWGN (every config uses the
+                           reference's real-only noise), 1e9 symbol-SNR evaluations in TOTAL (6.25e7
+                           symbols/point x 16 points), split over the ranks (strong)
   frame                    the reference's own trial (sync, CFO, LS): the like-for-like line next
                            to the reference's trial loop on the host
 
@@ -56,9 +57,9 @@ WORKLOADS = {
            dict(est="ideal", noise="real", channel="awgn", conv="c", payload="random"), 1_000_000, "weak"),
     "c4": ("BASELINE configs[3]: c3's chain, 1e8 symbols/point in total, counter-range shards over the ranks, "
            "RCCL all-reduce of the int64 counters", _LS_AWGN, 100_000_000, "strong"),
-    "c5": ("BASELINE configs[4]: 4-tap Rayleigh + per-subcarrier ZF (LTF LS), complex AWGN, full BER/EVM sweep, "
+    "c5": ("BASELINE configs[4]: 4-tap Rayleigh + per-subcarrier ZF (LTF LS), real AWGN, full BER/EVM sweep, "
            "1e9 symbol-SNR evaluations in total (6.25e7 symbols/point x 16) over the ranks",
-           dict(est="ls", noise="complex", channel="rayleigh4", conv="c", payload="random", kappa=1.0),
+           dict(est="ls", noise="real", channel="rayleigh4", conv="c", payload="random"),
            62_500_000, "strong"),
     "frame": ("frame mode: OFDM.c Transmission_Over_Air + Receiver trials (sync, CFO, LS), reference message",
               dict(payload="message", noise="real", conv="c"), 1_000_000, "weak"),
@@ -157,7 +158,7 @@ def cpu_baseline(workload: str, seconds: float = 12.0) -> dict | None:
                        (QPSK_Modulator, ifft, gaussian_noise, Channel_Estimation, fft, AGC_Receiver,
                        QPSK_Demodulator; ref_harness.c ref_time_symbol_chain) over the same 16 SNR
                        points, the Tx built once per frame as the GPU re-uses its Tx batch (c5 adds
-                       a restated 4-tap channel and complex noise: the reference has none, D9).
+                       a restated 4-tap channel ahead of the noise: the reference has none, D9).
     The reference is single-threaded with global state, so the multi-core figure runs one process
     per core of the box's share; the one-thread figure is reported beside it.  Runs before the GPU
     is initialised."""
@@ -184,7 +185,7 @@ def cpu_baseline(workload: str, seconds: float = 12.0) -> dict | None:
         job = lambda n, s: (n, s, rayleigh)                 # noqa: E731
         worker = _chain_worker
         what = (f"frames of the genie symbol chain composed from src/OFDM.c's stage functions "
-                f"({'4-tap Rayleigh + complex noise, ' if rayleigh else ''}LTF LS, 2 data symbols each) x "
+                f"({'4-tap Rayleigh, ' if rayleigh else ''}LTF LS, 2 data symbols each) x "
                 f"{len(SNR_GRID)} SNR points")
     cpu = cpu_model()
     P, visible = host_cores()
@@ -340,10 +341,11 @@ def main():
     bytes_per_unit = FRAME_CAPTURE_BYTES / 2 if frame_mode else BYTES_PER_SYMBOL_SNR
     res = pkg.SweepResult(SNR_GRID, c)
     pmc = load_pmc(args.workload)
-    # the receiver kernel this workload launches (ofdm_symbol.hip launch_rx): real-noise AWGN sweeps run
-    # the packed receiver (ofdm_rxpack.hip), the others the {E, D0, D1} LS / ideal receivers
+    # the receiver kernel this workload launches (ofdm_symbol.hip launch_rx): real-noise AWGN sweeps and
+    # real-noise LS Rayleigh sweeps run the packed receiver (ofdm_rxpack.hip), the others the {E, D0, D1}
+    # LS / ideal receivers
     kernel = ("frame_sync_kernel+frame_sym_kernel" if frame_mode
-              else "rx_pack_kernel" if kw.get("noise") == "real" and kw.get("channel") == "awgn"
+              else "rx_pack_kernel" if kw.get("noise") == "real" and (kw.get("channel") == "awgn" or kw.get("est") == "ls")
               else ("rx_ls_kernel" if kw.get("est") == "ls" else "rx_ideal_kernel"))
     if pmc and "+".join(pmc.get("kernels", [pmc.get("kernel")])) != kernel:
         pmc = {}                      # a PMC pass of another kernel: not this run's instruction count

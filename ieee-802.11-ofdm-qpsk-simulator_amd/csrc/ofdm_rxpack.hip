@@ -1,4 +1,5 @@
-// ofdm_rxpack.hip -- K3c: the real-noise symbol-mode receivers (configs c2 / c3, the benchmark).
+// ofdm_rxpack.hip -- K3c: the real-noise symbol-mode receivers (configs c2 / c3 / c4, the benchmark, and
+// the LS receiver of c5's 4-tap Rayleigh channel, whose taps act on the clean spectra once per group).
 //
 // The AWGN the reference adds is real-only (OFDM.c:651, D7) and the receiver's fft() is linear
 // (OFDM.c:314-318), so the spectrum of a received window is the clean symbol's spectrum plus the
@@ -50,9 +51,25 @@ __host__ __device__ constexpr int rev16(int m) { return ((m & 3) << 2) | (m >> 2
 // position of bin k (0..31) of the 32-point transform (radix-2 stage, then two 16-point dif4)
 __host__ __device__ constexpr int pos32(int k) { return (k & 1) ? 16 + rev16(k >> 1) : rev16(k >> 1); }
 
+// The 4-tap channel y[n] = sum_l h_l x[n - l] at FFT bin k of the (-1)^n-modulated window: the taps
+// reach 3 samples back, inside the 16-sample cyclic prefix, so over the receiver's window the convolution
+// is circular and FFT((-1)^n y[n])[k] = H'[k] FFT((-1)^n x[n])[k] with
+// H'[k] = sum_l (-1)^l h_l W64^{kl} (the same frequency response rx_ideal_kernel's ZF uses).
+template <int K>
+__device__ __forceinline__ float2 chan_bin(const float2 (&h)[4]) {
+    float2 H = h[0];
+    H = csub(H, twiddle<K * 1, false>(h[1]));
+    H = cadd(H, twiddle<K * 2, false>(h[2]));
+    return csub(H, twiddle<K * 3, false>(h[3]));
+}
+
 // Group prologue: clean spectrum of symbol `s` (window rows 16..79 of the Tx batch, times (-1)^n for
 // fft(), OFDM.c:314-318) -> the 24 bin pairs (C[k], C[64 - k]) of spec[p][half][frame].
-__device__ __forceinline__ void clean_spectrum(const RxArgs &a, int64_t s, float4 *spec_col /* &spec[0][half][f] */) {
+// FADE (4-tap Rayleigh, taps h of the symbol's frame): the faded spectrum H'[k] C[k]; both lanes of a frame
+// also store the frame's faded LTF-pair spectrum H'[k] FFT(2T)[k] to `ece_col` (the same value: no branch).
+template <bool FADE>
+__device__ __forceinline__ void clean_spectrum(const RxArgs &a, int64_t s, float4 *spec_col /* &spec[0][half][f] */,
+                                               const float2 (&h)[4], float4 *ece_col, const float4 *ce) {
     gcf2 *src = (gcf2 *)(a.tx + 16 * a.pitch + s);
     int P = (int)a.pitch;
     opaque(P);
@@ -73,8 +90,17 @@ __device__ __forceinline__ void clean_spectrum(const RxArgs &a, int64_t s, float
     static_for<0, PACK_PAIRS>([&](auto pc) {
         constexpr int p = decltype(pc)::value;
         constexpr int k = pair_bin(p);
-        const float2 c0 = x[digit_rev4(k)], c1 = x[digit_rev4(64 - k)];
+        float2 c0 = x[digit_rev4(k)], c1 = x[digit_rev4(64 - k)];
+        if constexpr (FADE) {
+            const float2 Hk = chan_bin<k>(h), Hm = chan_bin<64 - k>(h);
+            c0 = cmul(Hk, c0);
+            c1 = cmul(Hm, c1);
+            const float4 e = ce[p];
+            const float2 e0 = cmul(Hk, make_float2(e.x, e.y)), e1 = cmul(Hm, make_float2(e.z, e.w));
+            ece_col[p * PK_FRAMES] = make_float4(e0.x, e0.y, e1.x, e1.y);   // both symbol lanes: same value
+        }
         spec_col[p * 2 * PK_FRAMES] = make_float4(c0.x, c0.y, c1.x, c1.y);
+        if constexpr (FADE) sched_fence();     // one pair's channel response at a time (no hoisted H')
     });
 }
 
@@ -137,14 +163,21 @@ __device__ __forceinline__ Noise4 pack_noise(const PhiloxHead &hd, uint32_t c2, 
 
 // KIND 2: LS estimate from the LTF pair (E spectrum in LDS `ce`, noise from the packed 32-point FFT);
 // KIND 0: ideal channel knowledge (AWGN), Z = Y (times (-1)^bin for the C ifft convention, D5).
-template <int KIND, int CONV, bool DUMP>
+// CHAN (KIND 2 only): OFDM_CHAN_RAYLEIGH4 applies each frame's 4-tap channel to its clean spectra in the
+// group prologue (chan_bin): it does not depend on the SNR point, and the real noise is added after the
+// channel (OFDM.c:651 order), so the SNR loop is the AWGN loop with a per-frame E spectrum `fce`.
+template <int KIND, int CONV, int CHAN, bool DUMP>
 __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_IDEAL_WAVES) void rx_pack_kernel(RxArgs a) {
+    constexpr bool FADE = CHAN == OFDM_CHAN_RAYLEIGH4;
+    static_assert(!FADE || KIND == 2, "the packed Rayleigh receiver is the LS one");
+    constexpr bool EEL = KIND == 2 && EE_LDS_N > 0;
     __shared__ __attribute__((aligned(16))) float4 spec[PACK_PAIRS][2][PK_FRAMES];   // 48 KB: (C[k], C[64-k])
     __shared__ __attribute__((aligned(16))) float4 ce[PACK_PAIRS];                   // LS: FFT((-1)^n 2T[n])
+    __shared__ __attribute__((aligned(16))) float4 fce[FADE ? PACK_PAIRS : 1][FADE ? PK_FRAMES : 1];  // 24 KB: H' FFT(2T)
     __shared__ __attribute__((aligned(8))) uint32_t truth[3][PK_SYMS];               // pair-order words
     __shared__ unsigned long long sacc[OFDM_MAX_SNR][5];         // flush_lanes' five slots per SNR point
     __shared__ uint32_t pf_dummy[64];                             // L2 warm-up destination (never read)
-    __shared__ __attribute__((aligned(8))) float2 eel[KIND == 2 ? 4 : 1][KIND == 2 && EE_LDS_N > 0 ? EE_LDS_N : 1][KIND == 2 ? 64 : 1];
+    __shared__ __attribute__((aligned(8))) float2 eel[EEL ? 4 : 1][EEL ? EE_LDS_N : 1][EEL ? 64 : 1];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);      // wave-uniform: the SNR loop runs on SGPRs
     for (int i = tid; i < a.n_snr * 5; i += blockDim.x) (&sacc[0][0])[i] = 0ull;
@@ -208,7 +241,13 @@ __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_
 #else
         if (t < PK_SYMS) {
 #endif
-            clean_spectrum(a, grp * PK_SYMS + t, &spec[0][t & 1][t >> 1]);
+            float2 h[4];
+            if constexpr (FADE) {
+                const uint64_t ff = a.first_frame + (uint64_t)(grp * PK_FRAMES + (t >> 1));
+                channel_taps((uint32_t)ff, (uint32_t)(ff >> 32), a.k0, a.k1, h);
+            }
+            clean_spectrum<FADE>(a, grp * PK_SYMS + t, &spec[0][t & 1][t >> 1], h,
+                                 &fce[0][FADE ? t >> 1 : 0], ce);
         } else {
             const int j = t - PK_SYMS;
             const uint32_t *src = a.bits + 7 * a.pitch + grp * PK_SYMS + j;
@@ -254,7 +293,7 @@ __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_
             // z[m] = e'[2m] + j e'[2m+1] with e'[n] = (-1)^n e[n]; radix-2 stage fused, then two dif4<16>
             float2 z[64];      // z[0..31] used
             float2 ee[PACK_PAIRS];
-            lf2 *eew = (lf2 *)&eel[KIND == 2 ? wv : 0][0][KIND == 2 ? lane : 0];
+            lf2 *eew = (lf2 *)&eel[EEL ? wv : 0][0][EEL ? lane : 0];
             opaque(eew);
             if constexpr (KIND == 2) {
                 const float KE = noise_k(sigma * 1.41421356237309504880f);
@@ -340,7 +379,9 @@ __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_
             uint32_t db0[3] = {0u, 0u, 0u}, db1[3] = {0u, 0u, 0u};
             lcf4 *sp = (lcf4 *)&spec[0][0][lane];
             lcu2 *tw = (lcu2 *)&truth[0][2 * lane];
+            lcf4 *fp = (lcf4 *)&fce[0][FADE ? lane : 0];   // per-iteration address: the loads stay in the loop
             opaque(sp); opaque(tw);
+            if constexpr (FADE) opaque(fp);
             uint32_t sm;
             asm volatile("v_mov_b32 %0, 0x80000000" : "=v"(sm));
             float evm = 0.f;
@@ -370,7 +411,13 @@ __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_
                         const f2v v = eew[(p - EE_LDS_FIRST) * 64];
                         ex = v.x; ey = v.y;
                     }
-                    const float4 e4 = ce[p];
+                    float4 e4;
+                    if constexpr (FADE) {
+                        const f4v v = fp[p * PK_FRAMES];
+                        e4 = make_float4(v.x, v.y, v.z, v.w);
+                    } else {
+                        e4 = ce[p];
+                    }
                     const float2 Sk = make_float2(fmaf(0.5f, ex, e4.x), fmaf(0.5f, ey, e4.y));
                     const float2 Sm = make_float2(fmaf(0.5f, ex, e4.z), fmaf(-0.5f, ey, e4.w));
                     rk = __builtin_amdgcn_rcpf(fmaf(Sk.x, Sk.x, Sk.y * Sk.y));
@@ -425,31 +472,41 @@ __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_
     block_flush(a, sacc);
 }
 
-template <int KIND, int CONV>
+template <int KIND, int CONV, int CHAN = OFDM_CHAN_AWGN>
 static void launch_pack_t(hipStream_t st, const RxArgs &a, bool dump, unsigned grid) {
-    if (dump) hipLaunchKernelGGL((rx_pack_kernel<KIND, CONV, true>), dim3(grid), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((rx_pack_kernel<KIND, CONV, false>), dim3(grid), dim3(256), 0, st, a);
+    if (dump) hipLaunchKernelGGL((rx_pack_kernel<KIND, CONV, CHAN, true>), dim3(grid), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((rx_pack_kernel<KIND, CONV, CHAN, false>), dim3(grid), dim3(256), 0, st, a);
 }
 
+// Real-noise sweeps: AWGN with either estimator, and the 4-tap Rayleigh channel with the LS estimator
+// (the ideal-CSI Rayleigh ZF and every complex-noise sweep run the {E, D0, D1} / ideal receivers).
 bool rx_pack_applies(const ofdm_cfg &cfg) {
 #ifdef OFDM_RX_NO_PACK
     (void)cfg;
     return false;
 #else
-    return cfg.noise == OFDM_NOISE_REAL && cfg.channel == OFDM_CHAN_AWGN;
+    if (cfg.noise != OFDM_NOISE_REAL) return false;
+#ifndef OFDM_RX_NO_PACK_FADE
+    if (cfg.channel == OFDM_CHAN_RAYLEIGH4) return cfg.est == OFDM_EST_LS;
+#endif
+    return cfg.channel == OFDM_CHAN_AWGN;
 #endif
 }
 
 void launch_rx_pack(hipStream_t st, const RxArgs &a, const ofdm_cfg &cfg, bool dump, unsigned grid) {
-    if (cfg.est == OFDM_EST_LS) launch_pack_t<2, OFDM_CONV_C>(st, a, dump, grid);           // conv via a.ltf
+    if (cfg.est == OFDM_EST_LS && cfg.channel == OFDM_CHAN_RAYLEIGH4)
+        launch_pack_t<2, OFDM_CONV_C, OFDM_CHAN_RAYLEIGH4>(st, a, dump, grid);           // conv via a.ltf
+    else if (cfg.est == OFDM_EST_LS) launch_pack_t<2, OFDM_CONV_C>(st, a, dump, grid);
     else if (cfg.conv == OFDM_CONV_C) launch_pack_t<0, OFDM_CONV_C>(st, a, dump, grid);
     else launch_pack_t<0, OFDM_CONV_MATLAB>(st, a, dump, grid);
 }
 
 int rx_pack_grid(const ofdm_cfg &cfg, int64_t n_frames, int device) {
     const int64_t need = (n_frames + PK_FRAMES - 1) / PK_FRAMES;
-    const void *k = cfg.est == OFDM_EST_LS ? reinterpret_cast<const void *>(&rx_pack_kernel<2, OFDM_CONV_C, false>)
-                                           : reinterpret_cast<const void *>(&rx_pack_kernel<0, OFDM_CONV_C, false>);
+    const void *k = cfg.est != OFDM_EST_LS ? reinterpret_cast<const void *>(&rx_pack_kernel<0, OFDM_CONV_C, OFDM_CHAN_AWGN, false>)
+                  : cfg.channel == OFDM_CHAN_RAYLEIGH4
+                      ? reinterpret_cast<const void *>(&rx_pack_kernel<2, OFDM_CONV_C, OFDM_CHAN_RAYLEIGH4, false>)
+                      : reinterpret_cast<const void *>(&rx_pack_kernel<2, OFDM_CONV_C, OFDM_CHAN_AWGN, false>);
     int per_cu = 0, cus = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1) cus = 256;

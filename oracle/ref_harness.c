@@ -354,7 +354,7 @@ void ref_gaussian_noise(int n, float *out)
  * OFDM.c:1024-1069, restated), AGC_Receiver (852-871), QPSK_Demodulator (873-908), EVM and BER
  * sums (1104-1161, restated).  Noise var = kappa P_ref / 10^(snr/10).
  * rayleigh = 1 (config c5, no reference counterpart, D9): a 4-tap CN(0, 1/4) channel per frame
- * (restated) and complex noise of the same total variance, kappa = 1.
+ * (restated) ahead of the same real-only noise.
  * acc3 += {bit errors, bits, sum |z - d|^2}.  Returns wall seconds.
  */
 static unsigned long long g_bits_state = 0x9E3779B97F4A7C15ULL;
@@ -413,16 +413,12 @@ double ref_time_symbol_chain(const float *snr_db, int n_snr, int n_frames, int r
             memcpy(frame_tx, y, sizeof(y));
         }
         for (int q = 0; q < n_snr; ++q) {
-            const float kappa = rayleigh ? 1.0f : 0.4980f;
+            const float kappa = 0.4980f;
             const float sd = sqrtf(kappa * 52.0f / 4096.0f / powf(10.0f, snr_db[q] / 10.0f));
-            const float sc = rayleigh ? sd * 0.70710678f : sd;
             memcpy(frame_rx, frame_tx, sizeof(frame_rx));
-            for (int i = 192; i < 320; ++i)
-                frame_rx[i] += rayleigh ? sc * (gaussian_noise(0, 1) + I * gaussian_noise(0, 1)) : sd * gaussian_noise(0, 1);
+            for (int i = 192; i < 320; ++i) frame_rx[i] += sd * gaussian_noise(0, 1);
             for (int d = 0; d < D; ++d)
-                for (int i = 336 + 80 * d; i < 400 + 80 * d; ++i)
-                    frame_rx[i] += rayleigh ? sc * (gaussian_noise(0, 1) + I * gaussian_noise(0, 1))
-                                            : sd * gaussian_noise(0, 1);
+                for (int i = 336 + 80 * d; i < 400 + 80 * d; ++i) frame_rx[i] += sd * gaussian_noise(0, 1);
             Channel_Estimation(frame_rx, H, 480);
             for (int d = 0; d < D; ++d) {
                 Slice_Repeater(frame_rx, rx_time[d], 0, 336 + 80 * d, 400 + 80 * d, 1);

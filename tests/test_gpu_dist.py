@@ -47,11 +47,12 @@ def test_c4_rank_shard_equals_halves(engine, pkg):
 
 
 def test_c5_rank_shard_equals_halves(engine, pkg):
-    """C5: 1e9 symbol-SNR evaluations on 8 GPUs -> 3.90625e6 frames per rank (4-tap Rayleigh, complex AWGN)."""
+    """C5: 1e9 symbol-SNR evaluations on 8 GPUs -> 3.90625e6 frames per rank (4-tap Rayleigh, real AWGN, LS:
+    the packed receiver with the channel on its clean spectra)."""
     from ofdm_amd import dist as odist
     frames_total = 1_000_000_000 // 16 // 2
     a, b = odist.shard_range(frames_total, 5, 8)
-    cfg = pkg.make_cfg(noise="complex", channel="rayleigh4", kappa=1.0)
+    cfg = pkg.make_cfg(noise="real", channel="rayleigh4")
     whole = engine.symbol_sweep(cfg, SNR, b - a, first_frame=a)
     m = a + 1_234_567
     halves = engine.symbol_sweep(cfg, SNR, m - a, first_frame=a) + engine.symbol_sweep(cfg, SNR, b - m, first_frame=m)

@@ -155,6 +155,7 @@ CONFIGS = [
     dict(est="ideal", noise="none", channel="awgn", conv="c"),
     dict(est="ls", noise="none", channel="awgn", conv="c"),
     dict(est="ls", noise="real", channel="rayleigh4", conv="c"),
+    dict(est="ls", noise="real", channel="rayleigh4", conv="matlab"),
     dict(est="ideal", noise="complex", channel="rayleigh4", conv="c"),
     dict(est="ls", noise="complex", channel="rayleigh4", conv="matlab"),
 ]
@@ -268,6 +269,20 @@ def test_ls_mc_matches_oracle_mc(engine, oracle, pkg):
     o = oracle.symbol_sweep(oracle.cfg(), snrs, 0, n)
     assert np.all(np.abs(g[:, 3] - o[:, 3]) <= 3)
     assert np.all(np.abs(g[:, 7] - o[:, 7]) / o[:, 7] < 1e-4)
+
+
+def test_rayleigh_ls_mc_matches_oracle_mc(engine, oracle, pkg):
+    """C5's chain (4-tap Rayleigh, real AWGN, LTF LS + ZF; the packed receiver applies the channel to the
+    clean spectra as H'[k] C[k]) against the oracle's time-domain convolution on the same Philox streams,
+    including ragged groups (frames not a multiple of 64) and a non-zero first frame."""
+    snrs = [0.0, 10.0, 20.0, 30.0]
+    for f0, n in ((0, 4000), (98_765, 1_111)):
+        kw = dict(est="ls", noise="real", channel="rayleigh4", conv="c")
+        g = engine.symbol_sweep(pkg.make_cfg(**kw), snrs, n, first_frame=f0)
+        o = oracle.symbol_sweep(oracle.cfg(**kw), snrs, f0, n)
+        assert np.array_equal(g[:, :3], o[:, :3])
+        assert np.all(np.abs(g[:, 3] - o[:, 3]) <= np.maximum(3, 1e-3 * o[:, 3])), (g[:, 3], o[:, 3])
+        assert np.all(np.abs(g[:, 7] - o[:, 7]) / o[:, 7] < 1e-3), (g[:, 7], o[:, 7])
 
 
 def test_rayleigh_zf_diversity(engine, pkg):
