@@ -63,13 +63,22 @@ __device__ __forceinline__ float2 chan_bin(const float2 (&h)[4]) {
     return csub(H, twiddle<K * 3, false>(h[3]));
 }
 
+// Rayleigh prologue, waves 2-3 (idle while waves 0-1 run the clean FFTs): the channel response of one frame
+// at the 12 bin pairs of half HALF, (H'[k], H'[64 - k]) into col[p * PK_FRAMES] (&fce[0][frame]).
+template <int HALF>
+__device__ __forceinline__ void chan_pairs(const float2 (&h)[4], float4 *col) {
+    static_for<12 * HALF, 12 * HALF + 12>([&](auto pc) {
+        constexpr int p = decltype(pc)::value;
+        constexpr int k = pair_bin(p);
+        const float2 Hk = chan_bin<k>(h), Hm = chan_bin<64 - k>(h);
+        col[p * PK_FRAMES] = make_float4(Hk.x, Hk.y, Hm.x, Hm.y);
+        sched_fence();
+    });
+}
+
 // Group prologue: clean spectrum of symbol `s` (window rows 16..79 of the Tx batch, times (-1)^n for
 // fft(), OFDM.c:314-318) -> the 24 bin pairs (C[k], C[64 - k]) of spec[p][half][frame].
-// FADE (4-tap Rayleigh, taps h of the symbol's frame): the faded spectrum H'[k] C[k]; both lanes of a frame
-// also store the frame's faded LTF-pair spectrum H'[k] FFT(2T)[k] to `ece_col` (the same value: no branch).
-template <bool FADE>
-__device__ __forceinline__ void clean_spectrum(const RxArgs &a, int64_t s, float4 *spec_col /* &spec[0][half][f] */,
-                                               const float2 (&h)[4], float4 *ece_col, const float4 *ce) {
+__device__ __forceinline__ void clean_spectrum(const RxArgs &a, int64_t s, float4 *spec_col /* &spec[0][half][f] */) {
     gcf2 *src = (gcf2 *)(a.tx + 16 * a.pitch + s);
     int P = (int)a.pitch;
     opaque(P);
@@ -90,17 +99,8 @@ __device__ __forceinline__ void clean_spectrum(const RxArgs &a, int64_t s, float
     static_for<0, PACK_PAIRS>([&](auto pc) {
         constexpr int p = decltype(pc)::value;
         constexpr int k = pair_bin(p);
-        float2 c0 = x[digit_rev4(k)], c1 = x[digit_rev4(64 - k)];
-        if constexpr (FADE) {
-            const float2 Hk = chan_bin<k>(h), Hm = chan_bin<64 - k>(h);
-            c0 = cmul(Hk, c0);
-            c1 = cmul(Hm, c1);
-            const float4 e = ce[p];
-            const float2 e0 = cmul(Hk, make_float2(e.x, e.y)), e1 = cmul(Hm, make_float2(e.z, e.w));
-            ece_col[p * PK_FRAMES] = make_float4(e0.x, e0.y, e1.x, e1.y);   // both symbol lanes: same value
-        }
+        const float2 c0 = x[digit_rev4(k)], c1 = x[digit_rev4(64 - k)];
         spec_col[p * 2 * PK_FRAMES] = make_float4(c0.x, c0.y, c1.x, c1.y);
-        if constexpr (FADE) sched_fence();     // one pair's channel response at a time (no hoisted H')
     });
 }
 
@@ -241,13 +241,7 @@ __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_
 #else
         if (t < PK_SYMS) {
 #endif
-            float2 h[4];
-            if constexpr (FADE) {
-                const uint64_t ff = a.first_frame + (uint64_t)(grp * PK_FRAMES + (t >> 1));
-                channel_taps((uint32_t)ff, (uint32_t)(ff >> 32), a.k0, a.k1, h);
-            }
-            clean_spectrum<FADE>(a, grp * PK_SYMS + t, &spec[0][t & 1][t >> 1], h,
-                                 &fce[0][FADE ? t >> 1 : 0], ce);
+            clean_spectrum(a, grp * PK_SYMS + t, &spec[0][t & 1][t >> 1]);
         } else {
             const int j = t - PK_SYMS;
             const uint32_t *src = a.bits + 7 * a.pitch + grp * PK_SYMS + j;
@@ -278,8 +272,32 @@ __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_
                 }
 #endif
             }
+            if constexpr (FADE) {      // the group's channel responses, a frame's 24 pairs split over waves 2 / 3
+                const int fr = j & 63;
+                const uint64_t ff = a.first_frame + (uint64_t)(grp * PK_FRAMES + fr);
+                float2 h[4];
+                channel_taps((uint32_t)ff, (uint32_t)(ff >> 32), a.k0, a.k1, h);
+                if (j < 64) chan_pairs<0>(h, &fce[0][fr]);
+                else chan_pairs<1>(h, &fce[0][fr]);
+            }
         }
         __syncthreads();
+        if constexpr (FADE) {
+            // faded spectra: C <- H' C for both data symbols, and fce <- H' FFT(2T) (the frame's LS reference);
+            // one (pair, frame) per thread and step, so each H' is read and overwritten by one thread
+            for (int it = t; it < PACK_PAIRS * PK_FRAMES; it += 256) {
+                const int p = it >> 6, fr = it & 63;
+                const float4 H = fce[p][fr], c0 = spec[p][0][fr], c1 = spec[p][1][fr], e = ce[p];
+                const float2 Hk = make_float2(H.x, H.y), Hm = make_float2(H.z, H.w);
+                float2 u = cmul(Hk, make_float2(c0.x, c0.y)), v = cmul(Hm, make_float2(c0.z, c0.w));
+                spec[p][0][fr] = make_float4(u.x, u.y, v.x, v.y);
+                u = cmul(Hk, make_float2(c1.x, c1.y)); v = cmul(Hm, make_float2(c1.z, c1.w));
+                spec[p][1][fr] = make_float4(u.x, u.y, v.x, v.y);
+                u = cmul(Hk, make_float2(e.x, e.y)); v = cmul(Hm, make_float2(e.z, e.w));
+                fce[p][fr] = make_float4(u.x, u.y, v.x, v.y);
+            }
+            __syncthreads();
+        }
         const int64_t fl = grp * PK_FRAMES + lane;
         const bool valid = fl < a.n_frames;
         const uint64_t f = a.first_frame + (uint64_t)fl;
