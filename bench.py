@@ -216,21 +216,34 @@ def plan_chunks(first: int, frames: int) -> list[tuple[int, int]]:
 
 
 class PipelinedSymbolStep:
-    """One symbol-mode step: Tx + receiver of every chunk, the Tx of chunk k+1 on a second stream into the
-    other of two Tx batches while the receiver of chunk k runs (tools/overlap_ab.py: c3 +1.5-2.7 %, counters
-    bit-identical).  Events order each batch's reuse after the receiver that read it, and a step's Tx stream
-    after every receiver of the previous step."""
+    """One symbol-mode step: Tx + receiver of every chunk into two alternating Tx batches.  `fused`: the
+    receiver of chunk k builds chunk k+1's batch in its group prologues (ofdm_set_next_tx; the packed LS
+    receivers run it on the waves that idle while the clean spectra are transformed), one stream.  Otherwise
+    the Tx of chunk k+1 runs on a second stream while the receiver of chunk k runs (tools/overlap_ab.py:
+    c3 +1.5-2.7 %, counters bit-identical); events order each batch's reuse after the receiver that read it,
+    and a step's Tx stream after every receiver of the previous step."""
 
-    def __init__(self, torch, eng, cfg, chunks, counters, dev: int):
+    def __init__(self, torch, eng, cfg, chunks, counters, dev: int, fused: bool = False):
         self.torch, self.eng, self.cfg, self.chunks, self.counters = torch, eng, cfg, chunks, counters
         self.bufs = [eng.tx_buffers(max(n for _, n in chunks)) for _ in range(2 if len(chunks) > 1 else 1)]
         self.s_rx = torch.cuda.current_stream(dev)
         self.s_tx = torch.cuda.Stream(dev)
+        self.fused = fused
 
     def __call__(self):
         torch, eng, cfg, chunks, bufs = self.torch, self.eng, self.cfg, self.chunks, self.bufs
         s_rx, s_tx = self.s_rx, self.s_tx
         self.counters.zero_()
+        if self.fused:
+            # the packed LS receiver of chunk k builds chunk k+1's Tx batch on its blocks' idle prologue
+            # waves (ofdm_set_next_tx); one stream: the batch it overwrites was last read by receiver k-1
+            eng.set_stream(s_rx.cuda_stream)
+            eng.tx_frames(cfg, chunks[0][0], chunks[0][1], *bufs[0])
+            for k, (a, n) in enumerate(chunks):
+                if k + 1 < len(chunks):
+                    eng.set_next_tx(cfg, chunks[k + 1][0], chunks[k + 1][1], *bufs[(k + 1) % 2])
+                eng.rx_frames(cfg, *bufs[k % 2], a, n, SNR_GRID, self.counters)
+            return
         tx_done = [torch.cuda.Event() for _ in chunks]
         rx_done = [torch.cuda.Event() for _ in chunks]
         start = torch.cuda.Event()
@@ -262,6 +275,8 @@ def main():
                     help="override data symbols per SNR point (per GPU for weak workloads, total for strong)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--pipeline", choices=("auto", "fused", "streams"), default="auto",
+                    help="next chunk's Tx: fused into the LS receiver (auto for real-noise LS) or a second stream")
     args = ap.parse_args()
 
     rank0_single = int(os.environ.get("RANK", "0")) == 0 and int(os.environ.get("WORLD_SIZE", "1")) == 1
@@ -295,7 +310,11 @@ def main():
     frame_mode = args.workload == "frame"
     counters = eng.new_counters(len(SNR_GRID))
     chunks = plan_chunks(first, frames)
-    sym_step = PipelinedSymbolStep(torch, eng, cfg, chunks, counters, dev) if not frame_mode and chunks else None
+    # LS sweeps on real noise (c3, c4, c5): the next chunk's Tx fused into the receiver's group prologues;
+    # c2 (ideal CSI): the Tx of chunk k+1 on a second stream
+    fused = (kw.get("est") == "ls" and kw.get("noise") == "real") if args.pipeline == "auto" else args.pipeline == "fused"
+    sym_step = (PipelinedSymbolStep(torch, eng, cfg, chunks, counters, dev, fused=fused)
+                if not frame_mode and chunks else None)
 
     def step():
         if frame_mode:            # one trial = one frame of 2 data symbols; waveform cached on the device

@@ -48,6 +48,7 @@ _SIGS = {
     "ofdm_fft64": (C.c_int, [_V, _V, _V, C.c_int64, C.c_int, C.c_int]),
     "ofdm_tx_bytes": (C.c_int, [C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     "ofdm_tx_frames": (C.c_int, [_V, _V, C.c_uint64, C.c_int64, _V, _V]),
+    "ofdm_set_next_tx": (C.c_int, [_V, _V, C.c_uint64, C.c_int64, _V, _V]),
     "ofdm_rx_frames": (C.c_int, [_V, _V, _V, _V, C.c_uint64, C.c_int64, _V, C.c_int, _V]),
     "ofdm_rx_frames_dump": (C.c_int, [_V, _V, _V, _V, C.c_uint64, C.c_int64, _V, C.c_int, _V, _V, _V]),
     "ofdm_symbol_sweep": (C.c_int, [_V, _V, _V, C.c_int, C.c_uint64, C.c_int64, C.c_int64, _V]),

@@ -290,16 +290,16 @@ int ofdm_tx_bytes(int64_t n_frames, int64_t *tx_bytes, int64_t *bits_bytes) {
     return OFDM_OK;
 }
 
-int ofdm_tx_frames(ofdm_ctx *ctx, const ofdm_cfg *cfg, uint64_t first_frame, int64_t n_frames, void *d_tx,
-                   void *d_bits) {
-    Ctx *c = reinterpret_cast<Ctx *>(ctx);
+static int check_tx(Ctx *c, const ofdm_cfg *cfg, int64_t n_frames, const void *d_tx, const void *d_bits) {
     if (!c) return set_error(OFDM_E_ARG, "ctx is NULL");
     int rc = check_cfg(cfg);
     if (rc) return rc;
     if (n_frames < 0 || (n_frames && (!d_tx || !d_bits))) return set_error(OFDM_E_ARG, "bad tx buffers");
     if (n_frames > MAX_BATCH_FRAMES) return set_error(OFDM_E_ARG, "n_frames > %lld per batch", (long long)MAX_BATCH_FRAMES);
-    if (n_frames == 0) return OFDM_OK;
-    HIPOK(hipSetDevice(c->device));
+    return OFDM_OK;
+}
+
+static TxArgs tx_args(Ctx *c, const ofdm_cfg *cfg, uint64_t first_frame, int64_t n_frames, void *d_tx, void *d_bits) {
     TxArgs a{};
     a.tx = (float2 *)d_tx;
     a.bits = (uint32_t *)d_bits;
@@ -310,6 +310,17 @@ int ofdm_tx_frames(ofdm_ctx *ctx, const ofdm_cfg *cfg, uint64_t first_frame, int
     a.k1 = (uint32_t)(cfg->seed >> 32);
     a.payload = cfg->payload;
     a.table_frames = payload_table(cfg->payload, c->message, a.table);
+    return a;
+}
+
+int ofdm_tx_frames(ofdm_ctx *ctx, const ofdm_cfg *cfg, uint64_t first_frame, int64_t n_frames, void *d_tx,
+                   void *d_bits) {
+    Ctx *c = reinterpret_cast<Ctx *>(ctx);
+    int rc = check_tx(c, cfg, n_frames, d_tx, d_bits);
+    if (rc) return rc;
+    if (n_frames == 0) return OFDM_OK;
+    HIPOK(hipSetDevice(c->device));
+    const TxArgs a = tx_args(c, cfg, first_frame, n_frames, d_tx, d_bits);
     c->tic(Ctx::K_TX);
     launch_tx(c->stream, a, cfg->conv);
     c->toc();
@@ -317,9 +328,37 @@ int ofdm_tx_frames(ofdm_ctx *ctx, const ofdm_cfg *cfg, uint64_t first_frame, int
     return OFDM_OK;
 }
 
+int ofdm_set_next_tx(ofdm_ctx *ctx, const ofdm_cfg *cfg, uint64_t first_frame, int64_t n_frames, void *d_tx,
+                     void *d_bits) {
+    Ctx *c = reinterpret_cast<Ctx *>(ctx);
+    int rc = check_tx(c, cfg, n_frames, d_tx, d_bits);
+    if (rc) return rc;
+    c->nx_pending = n_frames > 0;
+    c->nx_cfg = *cfg;
+    c->nx_first = first_frame;
+    c->nx_n = n_frames;
+    c->nx_tx = d_tx;
+    c->nx_bits = d_bits;
+    return OFDM_OK;
+}
+
 static int rx_common(Ctx *c, const ofdm_cfg *cfg, const void *d_tx, const void *d_bits, uint64_t first_frame,
                      int64_t n_frames, const double *snr_db, int n_snr, void *d_counters, void *d_eq, void *d_dbits) {
     if (!c) return set_error(OFDM_E_ARG, "ctx is NULL");
+    // a pending ofdm_set_next_tx batch: fused into the packed receiver's group prologues when this call
+    // launches it, otherwise built by the Tx kernel right here (same stream, so it is ready in either case
+    // once this call's work is)
+    bool fuse_nx = false;
+    if (c->nx_pending) {
+        c->nx_pending = false;
+        fuse_nx = !d_eq && !d_dbits && n_frames > 0 && n_snr > 0 && cfg && check_cfg(cfg) == OFDM_OK &&
+                  rx_pack_applies(*cfg) && cfg->est == OFDM_EST_LS;
+        if (!fuse_nx) {
+            const int rt = ofdm_tx_frames(reinterpret_cast<ofdm_ctx *>(c), &c->nx_cfg, c->nx_first, c->nx_n,
+                                          c->nx_tx, c->nx_bits);
+            if (rt) return rt;
+        }
+    }
     int rc = check_cfg(cfg);
     if (rc) return rc;
     if (n_snr < 0 || (n_snr && !snr_db) || !d_counters) return set_error(OFDM_E_ARG, "bad snr/counters");
@@ -357,6 +396,10 @@ static int rx_common(Ctx *c, const ofdm_cfg *cfg, const void *d_tx, const void *
         HIPOK(hipMalloc(&a.stamps, 64));
         HIPOK(hipMemset(a.stamps, 0, 64));
 #endif
+        if (fuse_nx && q0 == 0) {
+            a.nx = tx_args(c, &c->nx_cfg, c->nx_first, c->nx_n, c->nx_tx, c->nx_bits);
+            a.nx_conv = c->nx_cfg.conv;
+        }
         if (!c->d_work) HIPOK(hipMalloc(&c->d_work, 256));
         a.work = (unsigned long long *)c->d_work;
         HIPOK(hipMemsetAsync(c->d_work, 0, sizeof(unsigned long long), c->stream));
@@ -436,6 +479,23 @@ int ofdm_symbol_sweep(ofdm_ctx *ctx, const ofdm_cfg *cfg, const double *snr_db, 
     int64_t f0, n0;
     chunk_of(0, &f0, &n0);
     if ((rc = ofdm_tx_frames(ctx, cfg, f0, n0, txbuf[0], bitbuf[0]))) return rc;
+    if (n_chunks > 1 && rx_pack_applies(*cfg) && cfg->est == OFDM_EST_LS) {
+        // the packed LS receiver of chunk k builds chunk k+1's batch in its group prologues (ofdm_set_next_tx),
+        // one stream: the batch it overwrites was last read by receiver k-1
+        for (int64_t k = 0; k < n_chunks; ++k) {
+            if (k + 1 < n_chunks) {
+                int64_t f1, n1;
+                chunk_of(k + 1, &f1, &n1);
+                if ((rc = ofdm_set_next_tx(ctx, cfg, f1, n1, txbuf[(k + 1) & 1], bitbuf[(k + 1) & 1]))) return rc;
+            }
+            int64_t fk, nk;
+            chunk_of(k, &fk, &nk);
+            if ((rc = ofdm_rx_frames(ctx, cfg, txbuf[k & 1], bitbuf[k & 1], fk, nk, snr_db, n_snr, c->d_cnt))) return rc;
+        }
+        HIPOK(hipMemcpyAsync(counters, c->d_cnt, cbytes, hipMemcpyDeviceToHost, c->stream));
+        HIPOK(hipStreamSynchronize(c->stream));
+        return OFDM_OK;
+    }
     for (int64_t k = 0; k < n_chunks; ++k) {
         if (k + 1 < n_chunks) {                                  // Tx of chunk k+1 into the other batch
             if (k >= 1) HIPOK(hipStreamWaitEvent(c->tx_stream, c->ev_rx[(k - 1) & 1], 0));   // chunk k-1 read it

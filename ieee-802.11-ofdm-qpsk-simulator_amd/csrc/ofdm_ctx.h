@@ -32,6 +32,12 @@ struct Ctx {
     void *d_tx2 = nullptr, *d_bits2 = nullptr;
     size_t cap_tx2 = 0, cap_bits2 = 0;
     hipStream_t tx_stream = nullptr;
+    // ofdm_set_next_tx: a Tx batch the next ofdm_rx_frames call builds (fused into the packed receiver)
+    bool nx_pending = false;
+    ofdm_cfg nx_cfg{};
+    uint64_t nx_first = 0;
+    int64_t nx_n = 0;
+    void *nx_tx = nullptr, *nx_bits = nullptr;
     hipEvent_t ev_start = nullptr, ev_tx[2] = {nullptr, nullptr}, ev_rx[2] = {nullptr, nullptr};
     void *d_wave = nullptr;
     void *d_work = nullptr;          // K3c's work-item counter (one receiver launch in flight per context)

@@ -56,6 +56,8 @@ struct RxArgs {
     int64_t dump_frames;               // leading dimension of the dumps (frames)
     unsigned long long *stamps;        // OFDM_RX_STAMPS builds: cycles per receiver phase [5]
     unsigned long long *work;          // K3c: work items handed out past the first gridDim.x (zeroed per launch)
+    TxArgs nx;                         // K3c: the NEXT chunk's Tx batch, built in the group prologues (n_sym 0: none)
+    int32_t nx_conv;                   // its ifft convention
     float sigma[OFDM_MAX_SNR];
 };
 

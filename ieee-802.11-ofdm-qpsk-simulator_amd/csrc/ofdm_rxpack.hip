@@ -272,6 +272,19 @@ __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_
                 }
 #endif
             }
+            // the next chunk's Tx batch (ofdm_set_next_tx), one symbol per lane: group gg of this launch's
+            // sub-0 item builds the next batch's symbols [128 gg', 128 gg' + 128) for gg' = gg, gg + G, ...
+            // (its arguments are re-read through an opaque kernarg pointer: hoisted, the 40 words of TxArgs
+            // would be held in SGPRs across the item loop and spill)
+            using KArgs = const __attribute__((address_space(4))) RxArgs;
+            KArgs *ap = (KArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+            asm volatile("" : "+s"(ap));
+            if (KIND == 2 && ap->nx.n_sym > 0 && sub == 0) {     // LS receivers (the chunked benchmarks)
+                for (int64_t sidx = grp * PK_SYMS + j; sidx < ap->nx.n_sym; sidx += (int64_t)G * PK_SYMS) {
+                    if (ap->nx_conv == OFDM_CONV_C) tx_symbol<OFDM_CONV_C>(ap->nx, sidx);
+                    else tx_symbol<OFDM_CONV_MATLAB>(ap->nx, sidx);
+                }
+            }
             if constexpr (FADE) {      // the group's channel responses, a frame's 24 pairs split over waves 2 / 3
                 const int fr = j & 63;
                 const uint64_t ff = a.first_frame + (uint64_t)(grp * PK_FRAMES + fr);

@@ -274,62 +274,12 @@ __global__ __launch_bounds__(256) void fft64_quad_kernel(const float2 *__restric
 }
 
 // ======================================================================== K2: Tx builder
-// One lane = one data symbol: bits -> QPSK (OFDM.c:415-433) -> subcarrier map + pilots
-// (OFDM.c:523-548) -> ifft (OFDM.c:320-339, convention D5) -> CP (OFDM.c:559-565) -> HBM.
+// One lane = one data symbol (tx_symbol, ofdm_rxcommon.h: bits -> QPSK -> map + pilots -> ifft -> CP -> HBM).
 template <int CONV>
 __global__ __launch_bounds__(256, 3) void tx_symbols_kernel(TxArgs a) {
     const int64_t sidx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // symbol within batch
     if (sidx >= a.n_sym) return;
-    const uint64_t s = a.first_symbol + (uint64_t)sidx;
-    uint32_t w[3];
-    if (a.payload == OFDM_PAYLOAD_RANDOM) {
-        const uint4 o = philox10((uint32_t)s, (uint32_t)(s >> 32), 0u, STREAM_BITS, a.k0, a.k1);
-        w[0] = o.x; w[1] = o.y; w[2] = o.z;
-    } else {
-        const int r = (int)(s % (uint64_t)a.table_frames);
-        w[0] = a.table[3 * r]; w[1] = a.table[3 * r + 1]; w[2] = a.table[3 * r + 2];
-    }
-    float2 X[64];
-    static_for<0, 4>([&](auto gc) {
-        constexpr int g = decltype(gc)::value;
-        uint32_t wg[3] = {w[0], w[1], w[2]};
-        opaque(wg[0]); opaque(wg[1]); opaque(wg[2]);
-        static_for<0, 16>([&](auto pc) {
-            constexpr int i = 16 * (decltype(pc)::value >> 2) + 4 * g + (decltype(pc)::value & 3);
-            X[i] = tx_bin<CONV, i>(wg);
-        });
-        static_for<0, 4>([&](auto ic) { dif_stage1<true, 4 * g + decltype(ic)::value>(X); });
-        sched_fence();
-    });
-    // row-major batch: sample n of symbol sidx at tx[n * pitch + sidx]; the row base
-    // is wave-uniform, so each store is saddr + one per-lane offset
-    const uint32_t so = (uint32_t)sidx;
-    [[maybe_unused]] const int64_t P = a.pitch;
-    static_for<0, 4>([&](auto rc) {
-        constexpr int R = decltype(rc)::value;
-        dif_sub16<true, R>(X);
-        static_for<0, 16>([&](auto nc) {
-            constexpr int n = 4 * decltype(nc)::value + R;                   // time samples n & 3 == R
-            const float2 v = cscale(X[digit_rev4(n)], (n & 1) ? -1.0f / 64.0f : 1.0f / 64.0f);
-            gst((gf2 *)(a.tx + (16 + n) * P), so, v);
-            if constexpr (n >= 48) gst((gf2 *)(a.tx + (n - 48) * P), so, v);   // CP = last 16 samples
-        });
-        sched_fence();
-    });
-    a.bits[so] = w[0];
-    a.bits[P + so] = w[1];
-    a.bits[2 * P + so] = w[2];
-    // rows 3..6: the receivers' demap words (ofdm_rxcommon.h)
-    a.bits[3 * P + so] = demap_word<0>(w);
-    a.bits[4 * P + so] = demap_word<1>(w);
-    a.bits[5 * P + so] = demap_word<2>(w);
-    a.bits[6 * P + so] = demap_word<3>(w);
-    // rows 7..9: the packed real-noise receivers' pair-order words (ofdm_rxcommon.h pair_words)
-    uint32_t pw[3];
-    pair_words(w, pw);
-    a.bits[7 * P + so] = pw[0];
-    a.bits[8 * P + so] = pw[1];
-    a.bits[9 * P + so] = pw[2];
+    tx_symbol<CONV>(a, sidx);
 }
 
 // ======================================================================== K3: receiver chain

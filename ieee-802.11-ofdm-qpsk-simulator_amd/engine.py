@@ -107,6 +107,12 @@ class Engine:
               "tx_frames")
         return tx, bits
 
+    def set_next_tx(self, cfg: Cfg, first_frame: int, n_frames: int, tx, bits):
+        """The next rx_frames call also builds this Tx batch (ofdm_set_next_tx: fused into the packed
+        receiver, else a Tx launch ahead of it on the same stream)."""
+        check(self.lib, self.lib.ofdm_set_next_tx(self.ctx, C.byref(cfg), first_frame, n_frames, _ptr(tx), _ptr(bits)),
+              "set_next_tx")
+
     def new_counters(self, n_snr: int):
         torch = _torch()
         return torch.zeros((n_snr, abi.NCOUNTERS), dtype=torch.int64, device=f"cuda:{self.device}")

@@ -35,18 +35,50 @@ def test_plan_chunks(first, frames):
 
 
 @pytest.mark.gpu
-def test_pipelined_step_equals_symbol_sweep(engine, pkg):
+@pytest.mark.parametrize("fused", [False, True])
+@pytest.mark.parametrize("channel", ["awgn", "rayleigh4"])
+def test_pipelined_step_equals_symbol_sweep(engine, pkg, fused, channel):
     import torch
     b = _bench()
-    cfg = pkg.make_cfg(est="ls", noise="real", channel="awgn", conv="c", payload="random")
+    cfg = pkg.make_cfg(est="ls", noise="real", channel=channel, conv="c", payload="random")
     first, frames = 1000, b.PIPE_CHUNKS * b.MIN_PIPE_FRAMES + 77
     chunks = b.plan_chunks(first, frames)
     assert len(chunks) == b.PIPE_CHUNKS
     counters = engine.new_counters(len(b.SNR_GRID))
-    step = b.PipelinedSymbolStep(torch, engine, cfg, chunks, counters, 0)
+    step = b.PipelinedSymbolStep(torch, engine, cfg, chunks, counters, 0, fused=fused)
     for _ in range(2):                    # twice: the second step reuses both batches
         step()
     torch.cuda.synchronize()
     got = counters.cpu().numpy()
     want = engine.symbol_sweep(cfg, b.SNR_GRID, frames, first_frame=first)
     assert np.array_equal(got, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kw", [dict(conv="c", payload="random"), dict(conv="matlab", payload="message"),
+                                dict(conv="c", payload="tester", channel="rayleigh4")])
+def test_fused_next_tx_equals_tx_kernel(engine, pkg, kw):
+    """ofdm_set_next_tx: the batch the packed LS receiver builds in its group prologues is byte-identical to
+    the Tx kernel's, for batches with more and with fewer groups than the receiver's launch (ragged sizes),
+    and the receiver's own counters are unchanged by the extra work."""
+    import torch
+    cfg = pkg.make_cfg(est="ls", noise="real", **kw)
+    snr = [0.0, 10.0]
+    tx0, bits0 = engine.tx_frames(cfg, 5, 1000)
+    want_cnt = engine.rx_frames(cfg, tx0, bits0, 5, 1000, snr).cpu().numpy()
+    for f1, n1 in ((1005, 2001), (3006, 333), (7, 64)):       # 2001 frames: the loop over groups gg + G
+        tx_ref, bits_ref = engine.tx_frames(cfg, f1, n1)
+        tx, bits = engine.tx_buffers(n1)
+        tx.fill_(-1.0)
+        bits.fill_(-1)
+        engine.set_next_tx(cfg, f1, n1, tx, bits)
+        cnt = engine.rx_frames(cfg, tx0, bits0, 5, 1000, snr)
+        torch.cuda.synchronize()
+        assert np.array_equal(cnt.cpu().numpy(), want_cnt)
+        n_sym = (2 * n1 + 63) // 64 * 64
+        a = tx_ref.view(torch.uint8).cpu().numpy().reshape(80, -1)
+        g = tx.view(torch.uint8).cpu().numpy().reshape(80, -1)
+        assert np.array_equal(a[:, :8 * n_sym], g[:, :8 * n_sym]), (f1, n1)
+        a = bits_ref.cpu().numpy().reshape(10, -1)
+        g = bits.cpu().numpy().reshape(10, -1)
+        assert np.array_equal(a[:, :n_sym], g[:, :n_sym]), (f1, n1)
