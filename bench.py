@@ -403,6 +403,9 @@ def main():
                           "instr_per_unit": ipu, "kernel": kernel, "avg_launch_ms": rx_avg_s * 1e3,
                           "launches": rx_n, "units_per_launch": units_per_launch,
                           "pmc_source": "profiles/pmc_summary.json[%s]" % {"c4": "c3"}.get(args.workload, args.workload),
+                          **({"fused_tx": "the receiver launches of chunks 0..n-2 also build the next chunk's Tx "
+                                          "batch (ofdm_set_next_tx); their VALU and HBM counts include it"}
+                             if fused and len(chunks) > 1 else {}),
                           **issue_cap(pmc, units_per_launch * ipu / rx_avg_s / VALU_PEAK_PER_S)}
                          if ipu else
                          {"bound": "valu", "achieved": None, "peak": VALU_PEAK_PER_S, "unit": "wave-instr/s",
