@@ -56,13 +56,16 @@ def test_pipelined_step_equals_symbol_sweep(engine, pkg, fused, channel):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("kw", [dict(conv="c", payload="random"), dict(conv="matlab", payload="message"),
-                                dict(conv="c", payload="tester", channel="rayleigh4")])
+                                dict(conv="c", payload="tester", channel="rayleigh4"),
+                                dict(conv="c", payload="random", noise="complex"),     # not fused: Tx launch
+                                dict(conv="c", payload="random", est="ideal")])        # not fused: Tx launch
 def test_fused_next_tx_equals_tx_kernel(engine, pkg, kw):
     """ofdm_set_next_tx: the batch the packed LS receiver builds in its group prologues is byte-identical to
     the Tx kernel's, for batches with more and with fewer groups than the receiver's launch (ragged sizes),
-    and the receiver's own counters are unchanged by the extra work."""
+    and the receiver's own counters are unchanged by the extra work.  Receivers that do not fuse it launch
+    the Tx kernel first: same bytes."""
     import torch
-    cfg = pkg.make_cfg(est="ls", noise="real", **kw)
+    cfg = pkg.make_cfg(**{"est": "ls", "noise": "real", **kw})
     snr = [0.0, 10.0]
     tx0, bits0 = engine.tx_frames(cfg, 5, 1000)
     want_cnt = engine.rx_frames(cfg, tx0, bits0, 5, 1000, snr).cpu().numpy()
