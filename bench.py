@@ -88,6 +88,48 @@ def issue_cap(pmc: dict, frac: float) -> dict:
                                 % m["waves_per_simd"]}
 
 
+def certify_pmc(pmc: dict, kernel: str, lib_id: str | None) -> tuple[dict, str | None]:
+    """The PMC record only if it measured THIS build of THIS kernel: same kernel set and the same build id
+    (codeobj: hash of the kernels' gfx950 code + descriptors) as the library this run loaded.  Otherwise
+    ({}, reason): a stale instruction count never reaches the roofline."""
+    if not pmc:
+        return {}, "no PMC record for this workload"
+    if "+".join(pmc.get("kernels", [pmc.get("kernel")])) != kernel:
+        return {}, f"PMC record is of {pmc.get('kernels')}, this run launches {kernel}"
+    if lib_id is None:
+        return {}, "kernel not found in the loaded library's gfx950 code objects"
+    if pmc.get("build_id") != lib_id:
+        return {}, f"PMC record build id {pmc.get('build_id')} != loaded library's {lib_id} (stale record)"
+    return pmc, None
+
+
+def make_roofline(pmc: dict, lib_id: str | None, kernel: str, workload: str, units_per_launch: float,
+                  rx_avg_s: float, rx_n: int, fused_tx: bool) -> tuple[dict, float | None]:
+    """The VALU-issue roofline of the run's receiver: achieved = measured VALU wave-instructions per unit
+    (SQ_INSTS_VALU / units, rocprofv3 --pmc, profiles/pmc_summary.json) x this run's units per launch / this
+    run's mean launch time (HIP events on the launch stream).  frac is null unless the PMC record is
+    certified for the loaded build (certify_pmc).  Returns (roofline, measured HBM bytes per launch)."""
+    pmc, why = certify_pmc(pmc, kernel, lib_id)
+    ipu = pmc.get("valu_instr_per_unit")
+    tpu = pmc.get("hbm_bytes_per_unit")
+    traffic = tpu * units_per_launch if tpu else None
+    base = {"bound": "valu", "peak": VALU_PEAK_PER_S, "unit": "wave-instr/s", "traffic": traffic,
+            "traffic_unit": "HBM bytes per launch (PMC)", "kernel": kernel, "avg_launch_ms": rx_avg_s * 1e3,
+            "launches": rx_n, "units_per_launch": units_per_launch, "lib_build_id": lib_id,
+            "pmc_build_id": pmc.get("build_id")}
+    if not ipu:
+        return {**base, "achieved": None, "frac": None, "frac_null_reason": why or "no VALU count"}, traffic
+    achieved = units_per_launch * ipu / rx_avg_s
+    frac = achieved / VALU_PEAK_PER_S
+    model = pmc.get("issue_model")
+    cap = issue_cap(pmc, frac) if model and model.get("build_id") == lib_id else {}
+    return {**base, "achieved": achieved, "frac": frac, "instr_per_unit": ipu,
+            "pmc_source": "profiles/pmc_summary.json[%s]" % {"c4": "c3"}.get(workload, workload),
+            **({"fused_tx": "the receiver launches of chunks 0..n-2 also build the next chunk's Tx batch "
+                            "(ofdm_set_next_tx); their VALU and HBM counts include it"} if fused_tx else {}),
+            **cap}, traffic
+
+
 def cpu_model() -> str:
     try:
         for line in Path("/proc/cpuinfo").read_text().splitlines():
@@ -98,14 +140,35 @@ def cpu_model() -> str:
     return platform.processor() or platform.machine()
 
 
-def host_cores() -> tuple[int, int]:
-    """(cores this benchmark uses, CPUs visible).  The pool runs with the GPU box's per-GPU CPU
-    share (16); more visible CPUs belong to other jobs' GPUs and are not used."""
+def _cgroup_cpu_quota() -> tuple[float | None, str]:
+    """CPUs granted by the cgroup CPU quota (v2 cpu.max, v1 cfs_quota_us / cfs_period_us), or None."""
     try:
-        n = len(os.sched_getaffinity(0))
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            return int(q) / int(per), f"cgroup v2 cpu.max {q}/{per}"
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(Path("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read_text())
+        per = int(Path("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read_text())
+        if q > 0:
+            return q / per, f"cgroup v1 cfs quota {q}/{per}"
+    except (OSError, ValueError):
+        pass
+    return None, "no cgroup CPU quota"
+
+
+def host_cpu_share() -> dict:
+    """The host CPUs this job may use, derived rather than assumed: the scheduler affinity mask, capped by
+    the cgroup CPU quota when one is set.  Under torchrun the share belongs to the whole job (one node),
+    and local rank 0 times the reference on all of it while the other ranks wait at the rendezvous."""
+    try:
+        aff = len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover
-        n = os.cpu_count() or 1
-    return max(1, min(16, n)), n
+        aff = os.cpu_count() or 1
+    quota, src = _cgroup_cpu_quota()
+    cores = aff if quota is None else max(1, min(aff, int(quota)))
+    return {"cores": cores, "affinity": aff, "quota": quota, "source": src, "visible": os.cpu_count() or aff}
 
 
 def _trial_worker(args):
@@ -118,9 +181,9 @@ def _trial_worker(args):
 
 def _chain_worker(args):
     """The symbol chain built from the reference's stage functions: (symbol-SNR units, seconds, BER)."""
-    n, seed, rayleigh = args
+    n, seed, rayleigh, ideal = args
     from oracle import RefLib  # noqa: PLC0415  (bench.py's cpu_baseline leg only)
-    t, acc = RefLib().time_symbol_chain(SNR_GRID, n, rayleigh=rayleigh, seed=seed)
+    t, acc = RefLib().time_symbol_chain(SNR_GRID, n, rayleigh=rayleigh, seed=seed, ideal=ideal)
     return 2 * n * len(SNR_GRID), t, float(acc[0] / max(acc[1], 1))
 
 
@@ -150,18 +213,20 @@ def _parallel(worker, jobs) -> tuple[float, float, list]:
     return sum(o[0][0] for o in out), wall, [o[0] for o in out]
 
 
-def cpu_baseline(workload: str, seconds: float = 12.0) -> dict | None:
+def cpu_baseline(workload: str, seconds: float = 12.0, share: dict | None = None) -> dict | None:
     """The reference itself (oracle/_ref/libofdm_ref.so, the unmodified OFDM.c built with gcc -O2,
     kind "reference") timed on this host, on the workload's own chain:
       frame            its trial loop (Transmission_Over_Air + Receiver, OFDM.c:1206-1217) at 10 dB;
-      c2/c3/c4/c5      the genie symbol chain of the GPU sweep composed from its stage functions
+      c3/c4/c5         the genie symbol chain of the GPU sweep composed from its stage functions
                        (QPSK_Modulator, ifft, gaussian_noise, Channel_Estimation, fft, AGC_Receiver,
                        QPSK_Demodulator; ref_harness.c ref_time_symbol_chain) over the same 16 SNR
                        points, the Tx built once per frame as the GPU re-uses its Tx batch (c5 adds
-                       a restated 4-tap channel ahead of the noise: the reference has none, D9).
+                       a restated 4-tap channel ahead of the noise: the reference has none, D9);
+      c2               the same chain with the known channel (ideal CSI): no per-SNR Channel_Estimation,
+                       as the GPU's ideal-CSI receiver has none.
     The reference is single-threaded with global state, so the multi-core figure runs one process
-    per core of the box's share; the one-thread figure is reported beside it.  Runs before the GPU
-    is initialised."""
+    per CPU of the job's host share (host_cpu_share: affinity capped by the cgroup quota); the
+    one-thread figure is reported beside it.  Runs before the GPU is initialised."""
     try:
         from oracle import RefLib  # noqa: PLC0415  (bench.py's cpu_baseline leg only)
         ref = RefLib()
@@ -170,6 +235,7 @@ def cpu_baseline(workload: str, seconds: float = 12.0) -> dict | None:
                 "sample": f"unavailable: {e}"}
     frame = workload == "frame"
     rayleigh = workload == "c5"
+    ideal = workload == "c2"
     if frame:
         t, _ = ref.time_trials(10.0, 50, 1)
         per = max(t / 50, 1e-6)
@@ -179,16 +245,18 @@ def cpu_baseline(workload: str, seconds: float = 12.0) -> dict | None:
         what = ("reference trials (Transmission_Over_Air + Receiver of src/OFDM.c, frame mode, 2 data symbols "
                 "each) at SNR 10 dB")
     else:
-        t, _ = ref.time_symbol_chain(SNR_GRID, 20, rayleigh=rayleigh, seed=1)
+        t, _ = ref.time_symbol_chain(SNR_GRID, 20, rayleigh=rayleigh, seed=1, ideal=ideal)
         per = max(t / 20, 1e-6)
-        one = lambda n, s: _chain_worker((n, s, rayleigh))  # noqa: E731
-        job = lambda n, s: (n, s, rayleigh)                 # noqa: E731
+        one = lambda n, s: _chain_worker((n, s, rayleigh, ideal))  # noqa: E731
+        job = lambda n, s: (n, s, rayleigh, ideal)                 # noqa: E731
         worker = _chain_worker
+        est = "known channel (ideal CSI)" if ideal else "LTF LS"
         what = (f"frames of the genie symbol chain composed from src/OFDM.c's stage functions "
-                f"({'4-tap Rayleigh, ' if rayleigh else ''}LTF LS, 2 data symbols each) x "
+                f"({'4-tap Rayleigh, ' if rayleigh else ''}{est}, 2 data symbols each) x "
                 f"{len(SNR_GRID)} SNR points")
     cpu = cpu_model()
-    P, visible = host_cores()
+    share = share or host_cpu_share()
+    P = share["cores"]
     n1 = max(20, int(seconds / 3 / per))
     u1, t1, m1 = one(n1, 7)
     single = {"value": u1 / t1, "unit": "OFDM symbols/s", "cores": 1, "kind": "reference",
@@ -198,12 +266,11 @@ def cpu_baseline(workload: str, seconds: float = 12.0) -> dict | None:
     return {"value": units / wall, "unit": "OFDM symbols/s", "cores": P, "kind": "reference",
             "sample": f"{P} x {n} {what} in {wall:.1f} s wall on {P} host processes started together "
                       f"(start-up untimed); mean BER {sum(r[2] for r in res) / P:.3g}",
-            "cpu_model": cpu, "cpus_visible": visible,
-            "cores_note": f"{P} = the GPU box's per-GPU CPU share; the other {max(visible - P, 0)} visible CPUs "
-                          "serve other GPUs and are not used",
-            "single_core": single,
-            "linear_all_visible_estimate": {"value": single["value"] * visible, "cores": visible,
-                                            "note": "1-thread rate x visible CPUs (extrapolated, not measured)"}}
+            "cpu_model": cpu, "cpus_visible": share["visible"],
+            "cores_source": f"{P} = min(sched_getaffinity {share['affinity']}, {share['source']})",
+            "cores_note": ("measured on the job's whole host share; CPUs outside it belong to other jobs "
+                           "and are not used (no extrapolation)"),
+            "single_core": single}
 
 
 def plan_chunks(first: int, frames: int) -> list[tuple[int, int]]:
@@ -265,6 +332,11 @@ class PipelinedSymbolStep:
             rx_done[k].record(s_rx)
 
 
+def wants_cpu_baseline(args) -> bool:
+    """Rank 0 of the job times the reference (any WORLD_SIZE); the others do not."""
+    return int(os.environ.get("RANK", "0")) == 0 and not args.no_cpu_baseline
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -279,14 +351,15 @@ def main():
                     help="next chunk's Tx: fused into the LS receiver (auto for real-noise LS) or a second stream")
     args = ap.parse_args()
 
-    rank0_single = int(os.environ.get("RANK", "0")) == 0 and int(os.environ.get("WORLD_SIZE", "1")) == 1
-    # host-side reference timing first, before anything touches the GPU (worker processes are spawned)
-    cpu = cpu_baseline(args.workload, args.cpu_seconds) if rank0_single and not args.no_cpu_baseline else None
+    # host-side reference timing first, before anything touches the GPU (worker processes are spawned).
+    # Under torchrun rank 0 (local rank 0 of the one node) times it before forming the process group; the
+    # other ranks wait at the rendezvous, so every N-GPU line carries the CPU figure of the same run
+    cpu = cpu_baseline(args.workload, args.cpu_seconds) if wants_cpu_baseline(args) else None
 
     import torch
     import torch.distributed as dist
     pkg = ofdm_pkg.load()
-    from ofdm_amd import abi, dist as odist
+    from ofdm_amd import abi, codeobj, dist as odist
 
     rank, world, local = odist.env_rank_world()
     # under torch.distributed.run (RANK set) the RCCL group is formed even for one rank, and the
@@ -366,13 +439,10 @@ def main():
     kernel = ("frame_sync_kernel+frame_sym_kernel" if frame_mode
               else "rx_pack_kernel" if kw.get("noise") == "real" and (kw.get("channel") == "awgn" or kw.get("est") == "ls")
               else ("rx_ls_kernel" if kw.get("est") == "ls" else "rx_ideal_kernel"))
-    if pmc and "+".join(pmc.get("kernels", [pmc.get("kernel")])) != kernel:
-        pmc = {}                      # a PMC pass of another kernel: not this run's instruction count
-    ipu = pmc.get("valu_instr_per_unit")
+    lib_id = codeobj.workload_build_id(abi.library_file(), args.workload)
+    roofline, traffic = make_roofline(pmc, lib_id, kernel, args.workload, units_per_launch, rx_avg_s, rx_n,
+                                      fused and len(chunks) > 1)
     hbm_alg = units_per_launch * bytes_per_unit / rx_avg_s / 1e9
-    tpu = pmc.get("hbm_bytes_per_unit") or (pmc["rx_hbm_bytes_per_launch"] / pmc["units_per_launch"]
-                                            if pmc.get("rx_hbm_bytes_per_launch") else None)
-    traffic = tpu * units_per_launch if tpu else None
     if rank == 0:
         line = {
             "metric": "OFDM symbols/sec (whole node) over BER-vs-SNR sweep; achieved HBM GB/s vs peak",
@@ -394,24 +464,8 @@ def main():
                        "parallelism": (f"dp{world} (counter-range shards, {scaling} scaling; 1 RCCL all-reduce of "
                                        "int64 counters per step)" if distributed
                                        else "1 process, no collective (not launched under torchrun)")},
-            # the binding roofline: VALU issue.  achieved = measured VALU wave-instructions
-            # per unit (SQ_INSTS_VALU / units, rocprofv3 --pmc, profiles/pmc_summary.json) x this run's
-            # units per launch / this run's mean launch time (HIP events on the launch stream)
-            "roofline": ({"bound": "valu", "achieved": units_per_launch * ipu / rx_avg_s, "peak": VALU_PEAK_PER_S,
-                          "unit": "wave-instr/s", "frac": units_per_launch * ipu / rx_avg_s / VALU_PEAK_PER_S,
-                          "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC)",
-                          "instr_per_unit": ipu, "kernel": kernel, "avg_launch_ms": rx_avg_s * 1e3,
-                          "launches": rx_n, "units_per_launch": units_per_launch,
-                          "pmc_source": "profiles/pmc_summary.json[%s]" % {"c4": "c3"}.get(args.workload, args.workload),
-                          **({"fused_tx": "the receiver launches of chunks 0..n-2 also build the next chunk's Tx "
-                                          "batch (ofdm_set_next_tx); their VALU and HBM counts include it"}
-                             if fused and len(chunks) > 1 else {}),
-                          **issue_cap(pmc, units_per_launch * ipu / rx_avg_s / VALU_PEAK_PER_S)}
-                         if ipu else
-                         {"bound": "valu", "achieved": None, "peak": VALU_PEAK_PER_S, "unit": "wave-instr/s",
-                          "frac": None, "traffic": traffic, "kernel": kernel, "avg_launch_ms": rx_avg_s * 1e3,
-                          "launches": rx_n, "units_per_launch": units_per_launch,
-                          "note": "no PMC pass recorded for this workload"}),
+            # the binding roofline: VALU issue (make_roofline)
+            "roofline": roofline,
             # HBM: the measured traffic (PMC) against the HBM peak is the HBM roofline fraction.  SURVEY
             # §8(d)'s streaming figure (652 B per unit, as if each symbol were re-read per SNR point) is kept
             # as a rate only: the kernels stage a symbol once per launch, so it is not traffic and has no

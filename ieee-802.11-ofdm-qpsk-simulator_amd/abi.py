@@ -108,11 +108,17 @@ def make_rx_opts(mode: str = "c", fixed_start: int = -1) -> RxOpts:
 
 
 _LIB = None
+_LIB_FILE: Path | None = None
+
+
+def library_file() -> Path:
+    """The shared object load_library() loaded (or would load): bench.py reads its kernels' build ids."""
+    return _LIB_FILE or Path(os.environ.get("OFDM_MI355X_LIB") or LIB_PATH)
 
 
 def load_library(path: Path | str | None = None) -> C.CDLL:
     """Load libofdm_mi355x.so (build it first with build_lib.build()).  Raises if absent."""
-    global _LIB
+    global _LIB, _LIB_FILE
     if _LIB is not None and path is None:
         return _LIB
     # OFDM_MI355X_LIB: load a variant build (tools/build_variants.py) instead of the default
@@ -135,7 +141,7 @@ def load_library(path: Path | str | None = None) -> C.CDLL:
     if lib.ofdm_abi_version() != ABI_VERSION:
         raise OfdmError(f"ABI mismatch: library {lib.ofdm_abi_version()} != {ABI_VERSION}")
     if path is None:
-        _LIB = lib
+        _LIB, _LIB_FILE = lib, p
     return lib
 
 

@@ -1,0 +1,104 @@
+"""Kernel build ids read from the shipped library's gfx950 code objects.
+
+A PMC record (profiles/pmc_summary.json) is a measurement of ONE build of a kernel: its VALU instruction
+count per unit is only valid for that machine code.  `kernel_build_id` hashes a kernel's code bytes and its
+kernel descriptor (VGPR/SGPR/LDS/scratch settings) straight from the .so, so the profiling run can stamp its
+record and bench.py can refuse a record whose id differs from the library it actually loaded.
+
+Pure Python (struct + hashlib) on the ELF layout: the .so's .hip_fatbin section holds one clang offload bundle
+per translation unit ("__CLANG_OFFLOAD_BUNDLE__", entry table of (offset, size, triple)); the gfx950 entry is
+an AMDGPU ELF64 code object whose .symtab names each kernel (STT_FUNC, its code) and `<kernel>.kd`
+(STT_OBJECT, its 64-byte descriptor).
+"""
+from __future__ import annotations
+
+import hashlib
+import re
+import struct
+from functools import lru_cache
+from pathlib import Path
+
+BUNDLE_MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+TARGET = "gfx950"
+
+# the kernels a workload's PMC record measures, as mangled-name fragments of their instantiations
+# (template arguments <KIND, CONV, CHAN, DUMP>; ofdm_rxpack.hip launch_rx_pack, ofdm_frame.hip)
+WORKLOAD_KERNELS = {
+    "c3": ("rx_pack_kernelILi2ELi0ELi0ELb0E",),
+    "c4": ("rx_pack_kernelILi2ELi0ELi0ELb0E",),
+    "c5": ("rx_pack_kernelILi2ELi0ELi1ELb0E",),
+    "c2": ("rx_pack_kernelILi0ELi0ELi0ELb0E",),
+    "frame": ("frame_sync_kernel", "frame_sym_kernelILb0E"),
+}
+
+
+def _bundles(blob: bytes):
+    """(triple, bytes) of every offload-bundle entry in the file."""
+    pos = blob.find(BUNDLE_MAGIC)
+    while pos >= 0:
+        n = struct.unpack_from("<Q", blob, pos + 24)[0]
+        o = pos + 32
+        for _ in range(n):
+            off, size, tlen = struct.unpack_from("<QQQ", blob, o)
+            triple = blob[o + 24:o + 24 + tlen].decode()
+            o += 24 + tlen
+            yield triple, blob[pos + off:pos + off + size]
+        pos = blob.find(BUNDLE_MAGIC, o)
+
+
+def _elf_symbols(elf: bytes):
+    """{name: bytes} of every sized FUNC / OBJECT symbol of an ELF64 little-endian code object."""
+    if elf[:4] != b"\x7fELF" or elf[4] != 2:
+        return {}
+    shoff, = struct.unpack_from("<Q", elf, 0x28)
+    shentsize, shnum = struct.unpack_from("<HH", elf, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQIIQQ", elf, shoff + i * shentsize) for i in range(shnum)]
+    out = {}
+    for s in secs:
+        if s[1] != 2:                      # SHT_SYMTAB
+            continue
+        strtab = secs[s[6]]
+        for i in range(s[5] // s[9]):
+            name_off, info, _, shndx, value, size = struct.unpack_from("<IBBHQQ", elf, s[4] + i * s[9])
+            if size == 0 or shndx == 0 or shndx >= len(secs) or (info & 0xF) not in (1, 2):
+                continue
+            so = strtab[4] + name_off
+            name = elf[so:elf.index(b"\0", so)].decode()
+            sec = secs[shndx]                # sh_addr, sh_offset: file offset of the symbol's bytes
+            start = sec[4] + (value - sec[3])
+            out[name] = elf[start:start + size]
+    return out
+
+
+@lru_cache(maxsize=8)
+def _symbols(path: str, mtime: float) -> dict:
+    blob = Path(path).read_bytes()
+    syms = {}
+    for triple, body in _bundles(blob):
+        if triple.endswith(TARGET):
+            syms.update(_elf_symbols(body))
+    return syms
+
+
+def kernel_symbols(lib_path) -> dict:
+    """{mangled name: code or descriptor bytes} of the gfx950 code objects inside the library."""
+    p = Path(lib_path)
+    return _symbols(str(p), p.stat().st_mtime)
+
+
+def kernel_build_id(lib_path, fragments) -> str | None:
+    """sha256 (first 16 hex digits) over the code and kernel descriptor of every kernel whose mangled name
+    contains one of `fragments`; None when no kernel matches."""
+    syms = kernel_symbols(lib_path)
+    names = sorted(n for n in syms if any(re.search(re.escape(f), n) for f in fragments))
+    if not names:
+        return None
+    h = hashlib.sha256()
+    for n in names:
+        h.update(n.encode() + b"\0" + syms[n])
+    return h.hexdigest()[:16]
+
+
+def workload_build_id(lib_path, workload: str) -> str | None:
+    frags = WORKLOAD_KERNELS.get(workload)
+    return kernel_build_id(lib_path, frags) if frags else None

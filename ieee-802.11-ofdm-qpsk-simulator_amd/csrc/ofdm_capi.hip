@@ -345,28 +345,29 @@ int ofdm_set_next_tx(ofdm_ctx *ctx, const ofdm_cfg *cfg, uint64_t first_frame, i
 static int rx_common(Ctx *c, const ofdm_cfg *cfg, const void *d_tx, const void *d_bits, uint64_t first_frame,
                      int64_t n_frames, const double *snr_db, int n_snr, void *d_counters, void *d_eq, void *d_dbits) {
     if (!c) return set_error(OFDM_E_ARG, "ctx is NULL");
+    // every argument check first: a call that fails them returns with a pending ofdm_set_next_tx batch still
+    // pending (nothing consumed, nothing launched)
+    int rc = check_cfg(cfg);
+    if (rc) return rc;
+    if (n_snr < 0 || (n_snr && !snr_db) || !d_counters) return set_error(OFDM_E_ARG, "bad snr/counters");
+    if (n_frames < 0 || (n_frames && (!d_tx || !d_bits))) return set_error(OFDM_E_ARG, "bad rx buffers");
+    if (n_frames > MAX_BATCH_FRAMES) return set_error(OFDM_E_ARG, "n_frames > %lld per batch", (long long)MAX_BATCH_FRAMES);
+    const bool dump = d_eq || d_dbits;
+    if (dump && (!d_eq || !d_dbits)) return set_error(OFDM_E_ARG, "dump needs both d_eq and d_dbits");
     // a pending ofdm_set_next_tx batch: fused into the packed receiver's group prologues when this call
     // launches it, otherwise built by the Tx kernel right here (same stream, so it is ready in either case
     // once this call's work is)
     bool fuse_nx = false;
     if (c->nx_pending) {
         c->nx_pending = false;
-        fuse_nx = !d_eq && !d_dbits && n_frames > 0 && n_snr > 0 && cfg && check_cfg(cfg) == OFDM_OK &&
-                  rx_pack_applies(*cfg) && cfg->est == OFDM_EST_LS;
+        fuse_nx = !dump && n_frames > 0 && n_snr > 0 && rx_pack_applies(*cfg) && cfg->est == OFDM_EST_LS;
         if (!fuse_nx) {
             const int rt = ofdm_tx_frames(reinterpret_cast<ofdm_ctx *>(c), &c->nx_cfg, c->nx_first, c->nx_n,
                                           c->nx_tx, c->nx_bits);
             if (rt) return rt;
         }
     }
-    int rc = check_cfg(cfg);
-    if (rc) return rc;
-    if (n_snr < 0 || (n_snr && !snr_db) || !d_counters) return set_error(OFDM_E_ARG, "bad snr/counters");
-    if (n_frames < 0 || (n_frames && (!d_tx || !d_bits))) return set_error(OFDM_E_ARG, "bad rx buffers");
-    if (n_frames > MAX_BATCH_FRAMES) return set_error(OFDM_E_ARG, "n_frames > %lld per batch", (long long)MAX_BATCH_FRAMES);
     if (n_frames == 0 || n_snr == 0) return OFDM_OK;
-    const bool dump = d_eq || d_dbits;
-    if (dump && (!d_eq || !d_dbits)) return set_error(OFDM_E_ARG, "dump needs both d_eq and d_dbits");
     HIPOK(hipSetDevice(c->device));
     const unsigned grid = (unsigned)rx_grid(*cfg, n_frames, c->device);
     for (int q0 = 0; q0 < n_snr; q0 += OFDM_MAX_SNR) {
@@ -445,6 +446,10 @@ int ofdm_symbol_sweep(ofdm_ctx *ctx, const ofdm_cfg *cfg, const double *snr_db, 
     if (n_snr < 0 || (n_snr && (!snr_db || !counters)) || n_frames < 0) return set_error(OFDM_E_ARG, "bad sweep args");
     if (n_snr == 0) return OFDM_OK;
     HIPOK(hipSetDevice(c->device));
+    if (c->nx_pending) {             // a batch queued by the caller: built now, before the sweep's own batches
+        c->nx_pending = false;
+        if ((rc = ofdm_tx_frames(ctx, &c->nx_cfg, c->nx_first, c->nx_n, c->nx_tx, c->nx_bits))) return rc;
+    }
     const size_t cbytes = (size_t)n_snr * OFDM_NCOUNTERS * sizeof(int64_t);
     if ((rc = c->ensure(&c->d_cnt, &c->cap_cnt, cbytes))) return rc;
     HIPOK(hipMemsetAsync(c->d_cnt, 0, cbytes, c->stream));

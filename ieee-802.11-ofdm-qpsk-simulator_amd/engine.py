@@ -259,6 +259,16 @@ class SweepResult:
         return np.where(c[:, abi.C_EVMDB_POST_FINITE] < c[:, abi.C_FRAMES], -np.inf, m)
 
     @property
+    def mean_finite_frame_evm_post_db(self) -> np.ndarray:
+        """mean of the per-frame post-slicer EVM_dB over the frames where it is finite (frames with >= 1
+        slicer error); -inf only where no frame had one.  A plottable companion of mean_frame_evm_post_db
+        for many trials per point (the reference's own statistic is -inf as soon as one trial is clean)."""
+        c = self.counters
+        fin = c[:, abi.C_EVMDB_POST_FINITE]
+        m = c[:, abi.C_EVMDB_POST_Q] / abi.EVM_Q_SCALE / np.maximum(fin, 1)
+        return np.where(fin > 0, m, -np.inf)
+
+    @property
     def sync_fail_rate(self) -> np.ndarray:
         c = self.counters
         return c[:, abi.C_SYNC_FAIL] / np.maximum(c[:, abi.C_FRAMES], 1)

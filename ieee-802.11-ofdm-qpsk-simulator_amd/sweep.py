@@ -12,8 +12,10 @@ Per-point values in the files.  Output_EVM_AGC.txt / Output_EVM_AGC_DB.txt hold,
 the MEAN over trials of the per-trial EVM_dB the reference writes for its one trial
 (OFDM.c:1126,1150); the post-slicer mean is -inf as soon as one trial had no slicer error, as the
 reference's own value for that trial is (ref_mc_curve.json's mean_evm_agc_db is the same
-statistic).  evm="pooled" writes 10 log10(sum|e|^2 / sum|d|^2) over all trials instead.  BER is
-errors / bits (= the mean per-trial BER: every trial carries the same bit count).
+statistic).  evm="finite" keeps that pre-slicer file and writes, after the slicer, the mean over the trials
+whose value is finite (trials with >= 1 slicer error; their count goes to the sidecar), so a many-trial
+run stays plottable above ~3 dB.  evm="pooled" writes 10 log10(sum|e|^2 / sum|d|^2) over all trials
+instead.  BER is errors / bits (= the mean per-trial BER: every trial carries the same bit count).
 
 Multi-GPU: launched under torchrun, each rank takes a contiguous share of the trials
 (dist.shard_range); reference_main() forms the process group (dist.init_from_env: RCCL, or gloo
@@ -59,7 +61,7 @@ def run_sweep(engine: Engine, snr_db, trials: int, mode: str = "frame", seed: in
 def reference_main(out_dir: str | Path = "data", trials: int = 1, mode: str = "frame", snr_db=REF_SNR,
                    seed: int = 0x80211A, device: int = 0, json_sidecar: bool = True, evm: str = "trial",
                    **kw) -> SweepResult:
-    if evm not in ("trial", "pooled"):
+    if evm not in ("trial", "finite", "pooled"):
         raise ValueError(evm)
     rank, world, local = dist.env_rank_world()
     if world > 1:
@@ -69,14 +71,17 @@ def reference_main(out_dir: str | Path = "data", trials: int = 1, mode: str = "f
         res = run_sweep(eng, snr_db, trials, mode=mode, seed=seed, rank=rank, world=world, **kw)
     wall = time.perf_counter() - t0
     if rank == 0:
-        pre, post = ((res.mean_frame_evm_db, res.mean_frame_evm_post_db) if evm == "trial"
-                     else (res.evm_pre_db, res.evm_post_db))
+        pre, post = {"trial": (res.mean_frame_evm_db, res.mean_frame_evm_post_db),
+                     "finite": (res.mean_frame_evm_db, res.mean_finite_frame_evm_post_db),
+                     "pooled": (res.evm_pre_db, res.evm_post_db)}[evm]
         write_reference_outputs(out_dir, res.snr_db, pre, post, res.ber)
         if json_sidecar:
             side = {"mode": mode, "trials_per_snr": trials, "world": world, "seed": seed, "wall_s": wall,
                     "evm_files": evm, "snr_db": res.snr_db.tolist(), "ber": res.ber.tolist(),
                     "mean_trial_evm_db": res.mean_frame_evm_db.tolist(),
                     "mean_trial_evm_post_db": [float(v) for v in res.mean_frame_evm_post_db],
+                    "mean_finite_trial_evm_post_db": [float(v) for v in res.mean_finite_frame_evm_post_db],
+                    "post_finite_trials": res.counters[:, abi.C_EVMDB_POST_FINITE].tolist(),
                     "evm_pre_db": res.evm_pre_db.tolist(),
                     "evm_post_db": [float(v) for v in res.evm_post_db], "sync_fail_rate": res.sync_fail_rate.tolist(),
                     "counters": res.counters.tolist()}
@@ -97,8 +102,9 @@ def main(argv=None):
     ap.add_argument("--conv", choices=["c", "matlab"], default="c")
     ap.add_argument("--payload", choices=["random", "message", "tester"])
     ap.add_argument("--message", help="MESSAGE payload text (default: OFDM.c:20), up to 96 characters")
-    ap.add_argument("--evm", choices=["trial", "pooled"], default="trial",
-                    help="EVM files: mean of per-trial EVM_dB (the reference's per-trial value) or pooled")
+    ap.add_argument("--evm", choices=["trial", "finite", "pooled"], default="trial",
+                    help="EVM files: mean of per-trial EVM_dB (the reference's statistic, -inf after the slicer "
+                         "once one trial is clean), the same with the post-slicer mean over finite trials, or pooled")
     ap.add_argument("--print-messages", action="store_true",
                     help="as OFDM.c:1167-1182: receive one capture per SNR point and print the decoded text")
     a = ap.parse_args(argv)

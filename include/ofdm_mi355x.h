@@ -136,7 +136,8 @@ int ofdm_rx_frames(ofdm_ctx *ctx, const ofdm_cfg *cfg, const void *d_tx, const v
  * (exactly what ofdm_tx_frames with the same arguments writes).  The packed real-noise LS receivers build
  * it in their group prologues on the block's otherwise idle waves; any other call launches ofdm_tx_frames on
  * the context's stream first.  The batch must not be the one that call reads.  One batch is pending at a
- * time (a second call replaces it). */
+ * time (a second call replaces it).  An rx call that fails its argument checks leaves the batch pending;
+ * ofdm_symbol_sweep builds a pending batch (Tx kernel, context stream) before its own work. */
 int ofdm_set_next_tx(ofdm_ctx *ctx, const ofdm_cfg *cfg, uint64_t first_frame, int64_t n_frames,
                      void *d_tx, void *d_bits);
 /* Per-symbol dump for parity tests: equalised data subcarriers d_eq [n_snr][n_frames][2][48] float2

@@ -235,6 +235,8 @@ class RefLib:
         L.ref_init.restype = C.c_int
         L.ref_time_trials.restype = C.c_double
         L.ref_time_trials.argtypes = [C.c_float, C.c_int, C.c_void_p]
+        L.ref_mc_trials.restype = C.c_double
+        L.ref_mc_trials.argtypes = [C.c_float, C.c_int, C.c_void_p]
         L.ref_toa.argtypes = [C.c_void_p, C.c_void_p, C.c_float, C.c_int]
         L.ref_trial.argtypes = [C.c_float, C.c_void_p]
         L.ref_seed.argtypes = [C.c_uint64]
@@ -313,11 +315,23 @@ class RefLib:
         t = self.lib.ref_time_trials(C.c_float(snr_db), int(n_trials), _p(acc))
         return t, acc
 
-    def time_symbol_chain(self, snr_db, n_frames: int, rayleigh: bool = False, seed: int = 0x80211A):
+    def mc_trials(self, snr_db: float, n_trials: int, seed: int):
+        """time_trials with per-trial statistics (ref_harness.c ref_mc_trials): (seconds, acc8) with
+        acc8 = [sum EVM_dB, sum EVM_AGC_dB, sum BER, sum BER^2, #BER>0, #BER>=1/4, sum EVM_dB^2,
+        #finite EVM_AGC_dB]."""
+        acc = np.zeros(8, np.float64)
+        self.lib.ref_seed(C.c_uint64(seed))
+        t = self.lib.ref_mc_trials(C.c_float(snr_db), int(n_trials), _p(acc))
+        return t, acc
+
+    def time_symbol_chain(self, snr_db, n_frames: int, rayleigh: bool = False, seed: int = 0x80211A,
+                          ideal: bool = False):
         """The genie symbol chain of the GPU sweep built from the reference's own stage functions
-        (ref_harness.c ref_time_symbol_chain); returns (seconds, [bit errors, bits, sum|z-d|^2])."""
+        (ref_harness.c ref_time_symbol_chain); returns (seconds, [bit errors, bits, sum|z-d|^2]).
+        ideal: the known channel instead of the per-SNR LTF estimate (config c2)."""
         snr = np.ascontiguousarray(snr_db, np.float32)
         acc = np.zeros(3, np.float64)
         self.lib.ref_seed(C.c_uint64(seed))
-        t = self.lib.ref_time_symbol_chain(_p(snr), len(snr), int(n_frames), int(rayleigh), _p(acc))
+        t = self.lib.ref_time_symbol_chain(_p(snr), len(snr), int(n_frames), int(rayleigh) | 2 * int(ideal),
+                                            _p(acc))
         return t, acc

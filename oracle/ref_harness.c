@@ -184,6 +184,35 @@ double ref_time_trials(float snr_db, int n_trials, double *res_sum3)
     return (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
 }
 
+/* The same trial loop with per-trial statistics for the Monte-Carlo fixture (tests/golden/gen_golden.py):
+ * acc8 = {Σ EVM_dB, Σ EVM_AGC_dB, Σ BER, Σ BER², trials with BER > 0, trials with BER >= 1/4,
+ *         Σ EVM_dB², trials with finite EVM_AGC_dB}.  The second moment gives the frame-clustered
+ * sampling error of the mean BER (a failed sync costs ~half of a trial's 192 bits at once). */
+double ref_mc_trials(float snr_db, int n_trials, double *acc8)
+{
+    int n = ref_init();
+    struct timespec t0, t1;
+    float res[3];
+    double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    float complex *ota = Allocate_Array_1D(n);
+    quiet_begin();
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int t = 0; t < n_trials; ++t) {
+        Transmission_Over_Air(g_tx, ota, snr_db, n);
+        Receiver(ota, n, data_frames_number, res);
+        acc[0] += res[0]; acc[1] += res[1]; acc[2] += res[2];
+        acc[3] += (double)res[2] * res[2];
+        acc[4] += res[2] > 0; acc[5] += res[2] >= 0.25f;
+        acc[6] += (double)res[0] * res[0];
+        acc[7] += isfinite(res[1]) != 0;
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    quiet_end();
+    free(ota);
+    if (acc8) memcpy(acc8, acc, sizeof(acc));
+    return (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
+}
+
 /*
  * Receiver() with its intermediate values exposed.  The orchestration below follows
  * Receiver() (OFDM.c:941-1165) statement for statement and calls the reference's own stage
@@ -353,8 +382,11 @@ void ref_gaussian_noise(int n, float *out)
  * 2 data windows), Channel_Estimation (OFDM.c:830-850), fft + ZF + demap (Receiver's inline loops
  * OFDM.c:1024-1069, restated), AGC_Receiver (852-871), QPSK_Demodulator (873-908), EVM and BER
  * sums (1104-1161, restated).  Noise var = kappa P_ref / 10^(snr/10).
- * rayleigh = 1 (config c5, no reference counterpart, D9): a 4-tap CN(0, 1/4) channel per frame
+ * flags bit 0 (config c5, no reference counterpart, D9): a 4-tap CN(0, 1/4) channel per frame
  * (restated) ahead of the same real-only noise.
+ * flags bit 1 (config c2, ideal CSI): the known channel instead of the LTF estimate -- H is taken once
+ * from Channel_Estimation of the noiseless frame (AWGN: the exact channel of the fft(ifft()) pair) and
+ * the per-SNR Channel_Estimation is skipped, as the GPU's ideal-CSI receiver skips it.
  * acc3 += {bit errors, bits, sum |z - d|^2}.  Returns wall seconds.
  */
 static unsigned long long g_bits_state = 0x9E3779B97F4A7C15ULL;
@@ -364,9 +396,10 @@ static unsigned int bits_next(void)
     return (unsigned int)(g_bits_state >> 11);
 }
 
-double ref_time_symbol_chain(const float *snr_db, int n_snr, int n_frames, int rayleigh, double *acc3)
+double ref_time_symbol_chain(const float *snr_db, int n_snr, int n_frames, int flags, double *acc3)
 {
     ref_init();
+    const int rayleigh = flags & 1, ideal = (flags >> 1) & 1;
     const int D = data_frames_number;     /* 2 for the reference message (OFDM.c:439) */
     const int pilot[4] = {1, 1, 1, -1};
     float complex T[64], ltf[64];
@@ -412,6 +445,7 @@ double ref_time_symbol_chain(const float *snr_db, int n_snr, int n_frames, int r
             }
             memcpy(frame_tx, y, sizeof(y));
         }
+        if (ideal) Channel_Estimation(frame_tx, H, 480);     /* known channel: noiseless LTF pair */
         for (int q = 0; q < n_snr; ++q) {
             const float kappa = 0.4980f;
             const float sd = sqrtf(kappa * 52.0f / 4096.0f / powf(10.0f, snr_db[q] / 10.0f));
@@ -419,7 +453,7 @@ double ref_time_symbol_chain(const float *snr_db, int n_snr, int n_frames, int r
             for (int i = 192; i < 320; ++i) frame_rx[i] += sd * gaussian_noise(0, 1);
             for (int d = 0; d < D; ++d)
                 for (int i = 336 + 80 * d; i < 400 + 80 * d; ++i) frame_rx[i] += sd * gaussian_noise(0, 1);
-            Channel_Estimation(frame_rx, H, 480);
+            if (!ideal) Channel_Estimation(frame_rx, H, 480);
             for (int d = 0; d < D; ++d) {
                 Slice_Repeater(frame_rx, rx_time[d], 0, 336 + 80 * d, 400 + 80 * d, 1);
                 fft(rx_time[d], rx_freq[d], 64);

@@ -85,3 +85,138 @@ def test_fused_next_tx_equals_tx_kernel(engine, pkg, kw):
         a = bits_ref.cpu().numpy().reshape(10, -1)
         g = bits.cpu().numpy().reshape(10, -1)
         assert np.array_equal(a[:, :n_sym], g[:, :n_sym]), (f1, n1)
+
+
+def _fake_pmc(build_id, kernel="rx_pack_kernel"):
+    return {"kernels": [kernel], "valu_instr_per_unit": 52.6, "hbm_bytes_per_unit": 90.0, "build_id": build_id,
+            "issue_model": {"cap_frac": 0.585, "waves_per_simd": 2, "build_id": build_id}}
+
+
+def test_roofline_needs_pmc_of_the_loaded_build(pkg):
+    """bench.py reports a VALU roofline fraction only from a PMC record stamped with the build id of the
+    library it loaded (codeobj: hash of the kernel's gfx950 code + descriptor); a mutated or missing id,
+    or a record of another kernel, gives frac null with the reason."""
+    from ofdm_amd import abi, codeobj
+    b = _bench()
+    lib_id = codeobj.workload_build_id(abi.library_file(), "c3")
+    assert lib_id and len(lib_id) == 16
+    assert codeobj.workload_build_id(abi.library_file(), "c4") == lib_id          # same receiver instance
+    assert len({codeobj.workload_build_id(abi.library_file(), w) for w in ("c2", "c3", "c5", "frame")}) == 4
+    args = ("rx_pack_kernel", "c3", 4e7, 3.4e-3, 16, True)
+    ok, traffic = b.make_roofline(_fake_pmc(lib_id), lib_id, *args)
+    assert ok["frac"] == pytest.approx(4e7 * 52.6 / 3.4e-3 / b.VALU_PEAK_PER_S)
+    assert ok["pmc_build_id"] == ok["lib_build_id"] == lib_id and traffic == 90.0 * 4e7
+    assert ok["issue_model_cap_frac"] == 0.585
+    mutated = lib_id[:-1] + ("0" if lib_id[-1] != "0" else "1")
+    for pmc, why in ((_fake_pmc(mutated), "stale"), (_fake_pmc(None), "stale"), ({}, "no PMC"),
+                     (_fake_pmc(lib_id, "rx_ls_kernel"), "launches")):
+        r, traffic = b.make_roofline(pmc, lib_id, *args)
+        assert r["frac"] is None and r["achieved"] is None and traffic is None
+        assert why in r["frac_null_reason"], r["frac_null_reason"]
+        assert "issue_model_cap_frac" not in r
+    # an issue-model record of another build is dropped, the PMC count of this build kept
+    pmc = _fake_pmc(lib_id)
+    pmc["issue_model"]["build_id"] = mutated
+    r, _ = b.make_roofline(pmc, lib_id, *args)
+    assert r["frac"] is not None and "issue_model_cap_frac" not in r
+
+
+def test_kernel_build_id_tracks_code_bytes(pkg, tmp_path):
+    """The id is a hash of the kernel's machine code: flipping one byte of it in a copy of the library
+    changes the id of that workload and no other's."""
+    from ofdm_amd import abi, codeobj
+    lib = abi.library_file()
+    syms = codeobj.kernel_symbols(lib)
+    name = next(n for n in syms if "rx_pack_kernelILi2ELi0ELi0ELb0E" in n and not n.endswith(".kd"))
+    blob = bytearray(lib.read_bytes())
+    at = blob.find(syms[name])
+    assert at > 0
+    blob[at + 100] ^= 0xFF
+    mod = tmp_path / "lib_mutated.so"
+    mod.write_bytes(bytes(blob))
+    assert codeobj.workload_build_id(mod, "c3") != codeobj.workload_build_id(lib, "c3")
+    assert codeobj.workload_build_id(mod, "c5") == codeobj.workload_build_id(lib, "c5")
+
+
+def test_host_cpu_share_is_derived(monkeypatch):
+    b = _bench()
+    monkeypatch.setattr(b, "_cgroup_cpu_quota", lambda: (3.0, "cgroup v2 cpu.max 300000/100000"))
+    s = b.host_cpu_share()
+    assert s["cores"] == min(3, s["affinity"]) and "cpu.max" in s["source"]
+    monkeypatch.setattr(b, "_cgroup_cpu_quota", lambda: (None, "no cgroup CPU quota"))
+    assert b.host_cpu_share()["cores"] == b.host_cpu_share()["affinity"]
+
+
+@pytest.mark.parametrize("workload", ["c3", "c2"])
+def test_torchrun_rank0_times_the_reference(reflib, monkeypatch, workload):
+    """Under torchrun (WORLD_SIZE=2) rank 0's line carries cpu_baseline with the derived core count; the
+    other rank does not time it.  c2 times the ideal-CSI chain (no per-SNR Channel_Estimation)."""
+    import argparse
+    b = _bench()
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setenv("RANK", "0")
+    assert b.wants_cpu_baseline(argparse.Namespace(no_cpu_baseline=False))
+    share = {"cores": 2, "affinity": 8, "quota": 2.0, "source": "cgroup v2 cpu.max 200000/100000", "visible": 8}
+    cpu = b.cpu_baseline(workload, seconds=0.3, share=share)
+    assert cpu["kind"] == "reference" and cpu["cores"] == 2 and cpu["value"] > 0
+    assert "cpu.max" in cpu["cores_source"] and cpu["single_core"]["cores"] == 1
+    assert ("known channel" in cpu["sample"]) == (workload == "c2")
+    monkeypatch.setenv("RANK", "1")
+    assert not b.wants_cpu_baseline(argparse.Namespace(no_cpu_baseline=False))
+
+
+def test_ideal_chain_skips_the_estimate(reflib):
+    """ref_time_symbol_chain with the known channel: at high SNR both chains are error-free; at 0 dB the LS
+    estimate's noise costs BER (the ideal chain's is lower), and the ideal chain is faster per frame."""
+    snr = np.array([0.0, 30.0])
+    t_ls, a_ls = reflib.time_symbol_chain(snr, 400, seed=5)
+    t_id, a_id = reflib.time_symbol_chain(snr, 400, seed=5, ideal=True)
+    assert a_id[1] == a_ls[1] == 400 * 2 * 96 * 2
+    assert a_id[0] < a_ls[0]
+
+
+@pytest.mark.gpu
+def test_pending_next_tx_survives_a_failed_rx_and_is_built_by_symbol_sweep(engine, pkg):
+    """ofdm_set_next_tx + an rx call that fails its argument checks: the batch stays pending (nothing
+    written), and the next valid rx call builds it.  ofdm_symbol_sweep builds a pending batch before its own
+    work.  Either way the bytes are the Tx kernel's."""
+    import ctypes as C
+    import torch
+    cfg = pkg.make_cfg(est="ls", noise="real", conv="c", payload="random")
+    tx0, bits0 = engine.tx_frames(cfg, 0, 256)
+    tx_ref, bits_ref = engine.tx_frames(cfg, 4096, 300)
+    torch.cuda.synchronize()
+
+    def fresh():
+        tx, bits = engine.tx_buffers(300)
+        tx.fill_(-1.0)
+        bits.fill_(-1)
+        torch.cuda.synchronize()
+        return tx, bits
+
+    def same(tx, bits):
+        torch.cuda.synchronize()
+        n = (2 * 300 + 63) // 64 * 64
+        a = tx_ref.view(torch.uint8).cpu().numpy().reshape(80, -1)[:, :8 * n]
+        g = tx.view(torch.uint8).cpu().numpy().reshape(80, -1)[:, :8 * n]
+        return np.array_equal(a, g) and np.array_equal(bits_ref.cpu().numpy().reshape(10, -1)[:, :n],
+                                                       bits.cpu().numpy().reshape(10, -1)[:, :n])
+
+    tx, bits = fresh()
+    engine.set_next_tx(cfg, 4096, 300, tx, bits)
+    cnt = engine.new_counters(2)
+    snr = np.array([0.0, 10.0])
+    eq = torch.zeros(8, device="cuda:0")
+    rc = engine.lib.ofdm_rx_frames_dump(engine.ctx, C.byref(cfg), C.c_void_p(tx0.data_ptr()),
+                                        C.c_void_p(bits0.data_ptr()), 0, 256, snr.ctypes.data_as(C.c_void_p), 2,
+                                        C.c_void_p(cnt.data_ptr()), C.c_void_p(eq.data_ptr()), None)
+    assert rc == -1                                      # OFDM_E_ARG: dump with d_eq only
+    torch.cuda.synchronize()
+    assert np.all(bits.cpu().numpy() == -1)              # the pending batch was not consumed
+    engine.rx_frames(cfg, tx0, bits0, 0, 256, snr, cnt)  # the next valid call builds it
+    assert same(tx, bits)
+
+    tx, bits = fresh()
+    engine.set_next_tx(cfg, 4096, 300, tx, bits)
+    engine.symbol_sweep(cfg, [5.0], 1000)                # flushes the pending batch first
+    assert same(tx, bits)

@@ -155,6 +155,13 @@ def test_mean_trial_evm_semantics(pkg):
     r = pkg.SweepResult(np.array([30.0, 0.0]), c)
     assert list(r.mean_frame_evm_db) == [-10.0, 2.0]
     assert np.isneginf(r.mean_frame_evm_post_db[0]) and r.mean_frame_evm_post_db[1] == 1.5
+    # --evm finite: the post-slicer mean over the finite trials only (-inf only with none finite)
+    c[0, abi.C_EVMDB_POST_Q], c[0, abi.C_EVMDB_POST_FINITE] = -30 << 20, 2
+    r = pkg.SweepResult(np.array([30.0, 0.0]), c)
+    assert np.isneginf(r.mean_frame_evm_post_db[0])
+    assert list(r.mean_finite_frame_evm_post_db) == [-15.0, 1.5]
+    c[0, abi.C_EVMDB_POST_FINITE] = 0
+    assert np.isneginf(pkg.SweepResult(np.array([30.0, 0.0]), c).mean_finite_frame_evm_post_db[0])
 
 
 def test_reference_symbol_chain_baseline_is_the_genie_workload(reflib):

@@ -16,6 +16,8 @@ step() {
   if fatal $rc; then echo "fatal rc=$rc in $name: stopping"; exit $rc; fi
 }
 BARGS=${BENCH_ARGS:---steps 1 --warmup 1 --no-cpu-baseline}
+# the build ids of the library this session profiles (tools/pmc_summary.py stamps its records with them)
+python3 tools/kernel_ids.py > "$OUT/kernel_ids.json" || exit 1
 step trace 300 rocprofv3 --kernel-trace --stats -d $OUT/pmc_trace -o run --output-format csv -- python3 bench.py $BARGS
 # counter groups, ';'-separated (one rocprofv3 --pmc pass each)
 GROUPS_DEFAULT="FETCH_SIZE;WRITE_SIZE;SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_SALU;GRBM_GUI_ACTIVE GRBM_COUNT;TCC_HIT_sum TCC_MISS_sum;SQ_INSTS_VALU_TRANS_F SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_VALU_FMA_F SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"

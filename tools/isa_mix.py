@@ -94,7 +94,11 @@ def main(argv):
         w = int(argv[argv.index("--waves") + 1]) if "--waves" in argv else 2
         out = ROOT / "profiles" / "pmc_summary.json"
         summary = json.loads(out.read_text())
+        sys.path.insert(0, str(ROOT / "tools"))
+        from kernel_ids import ids  # noqa: PLC0415
         summary[wl]["issue_model"] = {
+            # the assembly is compiled from the same sources and flags as the in-tree library: its build id
+            "build_id": ids()["ids"].get(wl),
             "kernel": name, "loop_valu": valu, "classes": dict(cls), "waves_per_simd": w,
             "priced_cycles": priced[w], "cap_frac": 2 * valu / priced[w],
             "source": "tools/isa_mix.py on the gfx950 assembly; class costs profiles/r01/ubench/"}

@@ -98,8 +98,20 @@ def main(argv):
         "trace": trace,
         "note": "FETCH_SIZE doubled (gfx950 reports half of wide streaming reads); sums over dispatches / units",
     }
-    if "issue_model" in summary.get(workload, {}):          # tools/isa_mix.py --record: a static-code figure
-        entry["issue_model"] = summary[workload]["issue_model"]
+    # the build id of the kernels measured: from the session's own kernel_ids.json (tools/gpu_profile.sh, written
+    # on the box from the library it profiled); bench.py refuses the record for any other build
+    ids_file = d / "kernel_ids.json"
+    if ids_file.exists():
+        entry["build_id"] = json.loads(ids_file.read_text())["ids"].get(workload)
+        entry["build_id_source"] = str(ids_file.relative_to(ROOT) if ids_file.is_relative_to(ROOT) else ids_file)
+    else:
+        sys.path.insert(0, str(ROOT / "tools"))
+        from kernel_ids import ids  # noqa: PLC0415
+        entry["build_id"] = ids()["ids"].get(workload)
+        entry["build_id_source"] = "in-tree library at summary time (no kernel_ids.json in the session)"
+    old = summary.get(workload, {}).get("issue_model")
+    if old and old.get("build_id") == entry["build_id"]:     # tools/isa_mix.py --record: a static-code figure
+        entry["issue_model"] = old
     summary[workload] = entry
     out.write_text(json.dumps(summary, indent=1, sort_keys=True))
     print(json.dumps(entry, indent=1))
