@@ -2,18 +2,19 @@
 //
 //   K4a frame_wave_kernel : Transmitter() (OFDM.c:467-618) -- preambles + data symbols, 2x zero
 //                           stuffing, 21-tap RRC, x10 repeat, mean power (OFDM.c:637-643).
-//   K4b frame_sync_kernel : one 128-thread block per (trial, SNR) item: capture (OFDM.c:945-955) + real
-//                           AWGN (OFDM.c:651) in LDS, Packet_Detection (659-683) as fma-chained sliding
-//                           sums with sign-bit crossings, Packet_Selection (685-771) as a DPP prefix max
-//                           + block min/max, the RRC matched filter only at the down-sampled instants the
-//                           receiver reads (965, 984-996), coarse/fine CFO (773-828) on wave 0, and the
-//                           rotated LTF / data windows handed to
+//   K4b frame_sync_kernel : one wave per (trial, SNR) item: capture (OFDM.c:945-955) + real AWGN
+//                           (OFDM.c:651) in LDS (real parts; the imaginary parts are the clean waveform's),
+//                           Packet_Detection (659-683) as fma-chained sliding sums with sign-bit crossings,
+//                           Packet_Selection (685-771) as a DPP prefix max + wave min/max, the RRC matched
+//                           filter only at the down-sampled instants the receiver reads (965, 984-996),
+//                           coarse/fine CFO (773-828) as wave reductions, and the rotated LTF / data
+//                           windows handed to
 //   K4b' frame_sym_kernel : the same register FFT + LS estimate + demap as symbol mode (830-1165).
 //   K4c ota_kernel        : Transmission_Over_Air() on a caller-provided waveform.
 //
-// The capture lives in LDS (24 KB per trial for the reference's 2-symbol message; frames carry 1..8
-// data symbols, ofdm_set_message); detection keeps only the >0.75 crossings as a bit mask, since
-// Packet_Selection needs nothing else (it re-reads Corr_Out only at front+230).
+// The capture's real parts live in LDS (12 KB per trial for the reference's 2-symbol message; frames carry
+// 1..8 data symbols, ofdm_set_message); detection keeps only the >0.75 crossings as per-lane bit masks,
+// since Packet_Selection needs nothing else (it re-reads Corr_Out only at front+230).
 #include "ofdm_internal.h"
 #include "ofdm_ctx.h"
 #include "ofdm_rxcommon.h"
@@ -57,6 +58,7 @@ struct FrameArgs {
     int32_t n_snr, q_base;
     int32_t cap_len, float_cfo, matlab, fixed_start, noise, wave_len, n_data, word_stats;
     int32_t fr_in_cap;              // fr[] inside the capture region (fr_in_capture)
+    int32_t imt_len, im_period;     // LDS table of the capture's imaginary parts: length, index period
     uint32_t k0, k1;
     uint32_t table[3 * FR_MAX_DATA];
     uint32_t dtable[4 * FR_MAX_DATA];   // demap words of the payload symbols (ofdm_rxcommon.h)
@@ -274,18 +276,6 @@ __global__ __launch_bounds__(256) void word_length_kernel(const float2 *x, int n
     }
 }
 
-__device__ __forceinline__ bool bit_at(const unsigned long long *m, int i) { return (m[i >> 6] >> (i & 63)) & 1ull; }
-// any set bit in [lo, hi] (inclusive, lo >= 0)
-__device__ __forceinline__ bool any_bits(const unsigned long long *m, int lo, int hi) {
-    for (int wd = lo >> 6; wd <= (hi >> 6); ++wd) {
-        unsigned long long w = m[wd];
-        if (wd == (lo >> 6)) w &= ~0ull << (lo & 63);
-        if (wd == (hi >> 6) && (hi & 63) != 63) w &= (1ull << ((hi & 63) + 1)) - 1ull;
-        if (w) return true;
-    }
-    return false;
-}
-
 // rotate by exp(-j 2 pi f Ts i): phase in revolutions evaluated in fp64 and range-reduced, so the
 // rotation matches OFDM.c:802,825 (double cexp of a float frequency) to fp32 rounding
 __device__ __forceinline__ float2 cfo_rot(float2 v, double f_ts, int i) {
@@ -317,119 +307,125 @@ __device__ __forceinline__ int needed_k(int j) {
     return 336 + 80 * (e >> 6) + (e & 63);
 }
 
-// ---------------------------------------------------------------- K4b: sync (one block per item)
-// LDS image of one trial (dynamic shared memory, sized per launch by frame_lds_bytes)
-#ifndef FRAME_SYNC_THREADS
-#define FRAME_SYNC_THREADS 128
+// ---------------------------------------------------------------- K4b: sync (one WAVE per item)
+// Every (trial, SNR) item is processed by one wave from capture to hand-off: packet detection, selection and
+// both CFO estimates are wave reductions (DPP / readlane), so the item needs no block barrier at all.  A block
+// of SYNC_WAVES waves only shares LDS: the imaginary parts of one waveform copy (the noise is real-only, D7:
+// a capture's imaginary part IS the clean waveform's, so each wave stores only the real parts of its
+// capture) and the per-SNR accumulators.  LDS per block (reference message): 4 x 12.1 KB captures + 4.4 KB
+// table = 53 KB, three blocks = 12 waves (3 per SIMD) per CU.
+#ifndef FRAME_SYNC_WAVES
+#define FRAME_SYNC_WAVES 4
 #endif
-constexpr int SYNC_THREADS = FRAME_SYNC_THREADS;   // the waves that share each trial's latency-bound phases
-constexpr int SYNC_WAVES = SYNC_THREADS / 64;
-static_assert(SYNC_WAVES >= 2 && SYNC_WAVES <= 4, "block reductions use 2..4 waves");
-// per-item scratch words after the accumulators: floats [0, 8) (block float sums), ints [8, 32)
-constexpr int RED_WORDS = 32, RED_I_MAX = 0, RED_I_PREFIX = 4, RED_I_MINMAX = 8, RED_I_NEXT = 20;
+constexpr int SYNC_WAVES = FRAME_SYNC_WAVES;
+constexpr int SYNC_THREADS = 64 * SYNC_WAVES;
+constexpr int IMT_EXT = 128;         // table slack past one waveform copy: a lane's longest contiguous read
+#ifndef FRAME_DET_B
+#define FRAME_DET_B 5               // detection positions per batch of LDS reads
+#endif
+constexpr int DET_B = FRAME_DET_B;
+// detection positions per lane and round: the largest odd chunk whose ceil(chunk / DET_B) batches fit one
+// 64-bit crossing mask (59 for DET_B = 5); at most 2 rounds (captures up to 64 x 2 x 59 + 47 samples)
+constexpr int det_max_chunk() {
+    int c = 63;
+    while ((c + DET_B - 1) / DET_B * DET_B > 64) c -= 2;
+    return c;
+}
+constexpr int DET_MAX_CHUNK = det_max_chunk();
+static_assert(64 * 2 * DET_MAX_CHUNK + 47 >= CAP_ABS_MAX, "two detection rounds cover every capture");
 #ifndef FRAME_ITEM_RUN
-#define FRAME_ITEM_RUN 4            // items per hand-out of the sync kernel's work counter
+#define FRAME_ITEM_RUN 4            // items per hand-out of the sync kernel's work counter (per wave)
 #endif
-constexpr int ACC_SLOTS = 12;       // per-SNR block accumulators: 9 counter sums + word-length min / max
-__host__ __device__ inline int cross_words(int cap_len) { return (cap_len - 47 + 63) / 64 + 1; }
-// capture region: cap_len + 8 samples, the capture starting at sample (rx_start & 3) so that every
-// Philox block of 4 samples is a 16-byte aligned pair of ds_write_b128
-__host__ __device__ inline int cap_region(int cap_len) { return (cap_len + 8 + 1) & ~1; }
-// The filtered frame fr[] goes into the part of the capture region the matched filter does not read:
-// it reads 2 nfr + 19 samples, so the unread prefix or suffix holds nfr samples whenever the region has
-// 4 nfr + 19 (every default capture).  Shorter user captures get fr[] after the scratch words instead.
-// (-3.8 KB per trial for the reference capture: 6 instead of 5 blocks per CU.)
+// per-SNR block accumulators: sync failures, OOB reads (and, with word_stats, the word-length min / max)
+__host__ __device__ inline int acc_slots(int word_stats) { return word_stats ? 4 : 2; }
+// capture region (floats): cap_len + 8, the capture starting at float (rx_start & 3) so that every Philox
+// block of 4 samples is one 16-byte aligned ds_write_b128; a multiple of 4 floats (16-byte aligned regions)
+__host__ __device__ inline int cap_region(int cap_len) { return (cap_len + 8 + 3) & ~3; }
+// The filtered frame fr[] (float2, indexed by frame sample) goes into the part of the capture region the
+// matched filter does not read: it reads 2 nfr + 19 floats, so the unread prefix or suffix holds the 2 nfr
+// floats of fr[] whenever the region has 6 nfr + 24.  Shorter user captures get fr[] after the region.
 __host__ __device__ inline bool fr_in_capture(int cap_len, int n_data) {
-    return cap_region(cap_len) >= 4 * fr_len(n_data) + 20;
+    return cap_region(cap_len) >= 6 * fr_len(n_data) + 24;
 }
-__host__ __device__ inline size_t frame_lds_bytes(int cap_len, int n_data, int n_snr) {
-#ifdef OFDM_FR_SEPARATE
-    const bool in_cap = false;
-#else
-    const bool in_cap = fr_in_capture(cap_len, n_data);
-#endif
-    return (size_t)cap_region(cap_len) * 8 + (size_t)cross_words(cap_len) * 8 + (size_t)n_snr * ACC_SLOTS * 8 +
-           RED_WORDS * 4 + (in_cap ? 0 : (size_t)fr_len(n_data) * 8);
+__host__ __device__ inline int wave_region_floats(int cap_len, int n_data) {
+    return cap_region(cap_len) + (fr_in_capture(cap_len, n_data) ? 0 : 2 * fr_len(n_data));
+}
+__host__ __device__ inline size_t frame_lds_bytes(int cap_len, int n_data, int n_snr, int imt_len, int word_stats) {
+    return (size_t)n_snr * acc_slots(word_stats) * 8 + (((size_t)imt_len * 4 + 15) & ~size_t(15)) +
+           (size_t)SYNC_WAVES * wave_region_floats(cap_len, n_data) * 4;
 }
 
-// block-wide exchange over the SYNC_WAVES waves, the wave partials combined in wave order
-// (min of a, max of b) over the waves in one exchange (scratch: 2 SYNC_WAVES slots).  LEAD: the barrier
-// that keeps the slots from being overwritten while an earlier exchange still reads them; the item
-// loop's slots were last read before the previous item's closing barrier, so it passes false.
-template <bool LEAD = true>
-__device__ __forceinline__ int2 block_minmax_i(int a, int b, int *red) {
-    a = wave_min_i(a);
-    b = wave_max_i(b);
-    if (LEAD) __syncthreads();
-    if ((threadIdx.x & 63) == 0) { red[2 * (threadIdx.x >> 6)] = a; red[2 * (threadIdx.x >> 6) + 1] = b; }
-    __syncthreads();
-    int2 t = make_int2(red[0], red[1]);
+// LDS ordering between the lanes of one wave (no block barrier: the other waves run other items)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// 21 contiguous LDS floats p[s .. s + 20] into x[20 - t] = p[s + t] order reversed (x[t] = sample n - t for
+// s = n - 20), as 10 ds_read_b64 + 1 ds_read_b32; ODD = s & 1 (uniform per item: the pairs are 8-byte aligned)
+template <int ODD>
+__device__ __forceinline__ void lds_read21(const float *p, int s, float (&x)[21]) {
+    const float2 *q = reinterpret_cast<const float2 *>(p + s + ODD);
 #pragma unroll
-    for (int w = 1; w < SYNC_WAVES; ++w) { t.x = min(t.x, red[2 * w]); t.y = max(t.y, red[2 * w + 1]); }
-    return t;
+    for (int m = 0; m < 10; ++m) {
+        const float2 w = q[m];                       // floats s + ODD + 2m, s + ODD + 2m + 1
+        x[20 - ODD - 2 * m] = w.x;
+        x[19 - ODD - 2 * m] = w.y;
+    }
+    x[ODD ? 20 : 0] = p[ODD ? s : s + 20];
 }
 
-#ifndef FRAME_SYNC_MINB
-#define FRAME_SYNC_MINB 3   // 3 waves/SIMD: +1.3 % (profiles/r01/ab/ab_frame_sync3.json)
+#ifndef FRAME_SYNC_MINW
+#define FRAME_SYNC_MINW 3   // waves per SIMD the VGPR budget targets (LDS holds 3 blocks of 4 waves per CU)
 #endif
-__global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kernel(FrameArgs a) {
+__global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kernel(FrameArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
     const int L = a.cap_len, Lc = L - 47;       // Packet_Detection length (OFDM.c:663)
     const int nfr = fr_len(a.n_data);
-    const int tid = threadIdx.x, lane = tid & 63;
-    float2 *rbase = reinterpret_cast<float2 *>(smem);
-    unsigned long long *cross = reinterpret_cast<unsigned long long *>(rbase + cap_region(L));
-    unsigned long long *acc = cross + cross_words(L);
-    float *redf = reinterpret_cast<float *>(acc + a.n_snr * ACC_SLOTS);
-    int *redi = reinterpret_cast<int *>(redf + 8);
-    float2 *const fr_sep = reinterpret_cast<float2 *>(redf + RED_WORDS);   // used when !fr_in_capture
-    float2 *fr = fr_sep;
-    for (int i = tid; i < a.n_snr * ACC_SLOTS; i += SYNC_THREADS) {
-        const int k = i % ACC_SLOTS;
-        acc[i] = k == 10 ? (unsigned long long)INT64_MAX : k == 11 ? (unsigned long long)INT64_MIN : 0ull;
+    const int ns = acc_slots(a.word_stats);
+    unsigned long long *acc = smem;                                           // [n_snr][ns]
+    float *imt = reinterpret_cast<float *>(acc + a.n_snr * ns);              // imaginary parts, [imt_len]
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float *rbase = imt + ((a.imt_len + 3) & ~3) + wv * wave_region_floats(L, a.n_data);
+    float2 *const fr_sep = reinterpret_cast<float2 *>(rbase + cap_region(L));   // when !fr_in_capture
+    for (int i = threadIdx.x; i < a.n_snr * ns; i += SYNC_THREADS) {
+        const int k = i % ns;
+        acc[i] = k == 2 ? (unsigned long long)INT64_MAX : k == 3 ? (unsigned long long)INT64_MIN : 0ull;
     }
-    // detection positions per lane (< 300, <= 64); odd, so the lanes' 8-byte LDS reads fall in
-    // distinct banks
-    const int chunk = ((Lc + SYNC_THREADS - 1) / SYNC_THREADS) | 1;
+    // the table: waveform mode imt[k] = Im wave[k mod nfilt] (every capture sample n reads imt[(rx_start + n)
+    // mod nfilt]; a lane's contiguous reads start below nfilt and run at most IMT_EXT past it); an external
+    // capture (ofdm_receiver, one item) its own imaginary parts, imt[n] = Im ext[n], zero past L
+    for (int k = threadIdx.x; k < a.imt_len; k += SYNC_THREADS)
+        imt[k] = a.ext ? (k < L ? a.ext[k].y : 0.f) : a.wave[k % a.im_period].y;
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
 #ifdef OFDM_FRAME_STAMPS
     unsigned long long stamp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long stamp_t = __builtin_amdgcn_s_memtime();
 #endif
-    // Items go out in runs of FRAME_ITEM_RUN: block b starts with run b, the runs past the first gridDim.x
-    // come from a per-launch atomic counter, so blocks that run fast take more runs.  Thread 0 fetches the
-    // next run at the first item of the current one (its wait on the atomic is paid once per run), every
-    // thread reads it after the capture barrier of the run's last item.  One atomic per item serialises on
-    // the counter's address at ~10 M/s, below the kernel's item rate.
-#ifndef OFDM_FRAME_STATIC_ITEMS
-    int64_t run_end = (int64_t)blockIdx.x * FRAME_ITEM_RUN + FRAME_ITEM_RUN;
-    for (int64_t i = run_end - FRAME_ITEM_RUN, inext = 0; i < a.n_items; i = inext) {
-#else
-    for (int64_t i = blockIdx.x, inext = 0; i < a.n_items; i = inext) {
-#endif
-#ifndef FRAME_HOIST_LANE
-        // lane-derived values (addresses, sample indices, fp64 instants) are re-derived per item instead of
-        // being hoisted out of the item loop and held in ~40 VGPRs across every phase
-        int tid = threadIdx.x;
-        opaque(tid);
-        const int lane = tid & 63;
-#endif
-#ifndef FRAME_HOIST_ARGS
-        // the kernel arguments are re-read per item (scalar loads from the kernarg segment through a pointer
-        // made opaque here) instead of being hoisted into ~100 SGPRs held across the item loop, most of
-        // which spilled to VGPR lanes and came back by v_readlane (a VALU op) at every use
+    // detection geometry: R rounds of 64 lanes x chunk positions (chunk odd: the lanes' LDS reads fall in
+    // distinct banks); one round for the reference capture (chunk 47)
+    const int R = (Lc + 64 * DET_MAX_CHUNK - 1) / (64 * DET_MAX_CHUNK);
+    const int chunk = ((Lc + 64 * R - 1) / (64 * R)) | 1;
+    // Items go out in runs of FRAME_ITEM_RUN per wave: wave gw starts with run gw, the runs past the first
+    // gridDim.x * SYNC_WAVES come from a per-launch atomic counter, so waves that run fast take more runs.
+    // Lane 0 fetches the next run at the first item of the current one (its wait is paid once per run).
+    const int nwaves = (int)gridDim.x * SYNC_WAVES;
+    int64_t run_end = ((int64_t)blockIdx.x * SYNC_WAVES + wv) * FRAME_ITEM_RUN + FRAME_ITEM_RUN;
+    int nxt = 0;
+    for (int64_t i = run_end - FRAME_ITEM_RUN; i < a.n_items;) {
+        // the kernel arguments are re-read per item (scalar loads through a pointer made opaque here)
+        // instead of being hoisted into SGPRs held across the item loop, which spill
         using KArgs = const __attribute__((address_space(4))) FrameArgs;
         KArgs *ap = (KArgs *)__builtin_amdgcn_kernarg_segment_ptr();
         asm volatile("" : "+s"(ap));
         KArgs &a = *ap;
-#endif
-#ifndef OFDM_FRAME_STATIC_ITEMS
-        if (threadIdx.x == 0 && i == run_end - FRAME_ITEM_RUN)
-            redi[RED_I_NEXT] = (int)gridDim.x + (int)atomicAdd(a.work, 1ull);
-#endif
+        if (lane == 0 && i == run_end - FRAME_ITEM_RUN) nxt = nwaves + (int)atomicAdd(a.work, 1ull);
         const int64_t g = a.item0 + i;
         int q;
         int64_t ti;
-        if ((uint64_t)g >> 32 == 0) {        // 32-bit division while it fits (~120 SALU less per item)
+        if ((uint64_t)g >> 32 == 0) {        // 32-bit division while it fits
             const uint32_t g32 = (uint32_t)g, d = (uint32_t)a.n_snr;
             ti = g32 / d;
             q = (int)(g32 - (uint32_t)ti * d);
@@ -441,106 +437,78 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
         const uint32_t t_lo = (uint32_t)t, t_hi = (uint32_t)(t >> 32), qs = (uint32_t)(a.q_base + q);
         const float sigma = a.sigma[q];
         const bool first_item = g == 0;
-        // ---- capture window (OFDM.c:945-955) + AWGN ----
+        const bool ext = a.ext && first_item;
+        // ---- capture window (OFDM.c:945-955) + AWGN: the real parts only ----
         int rx_start = a.fixed_start;
         if (rx_start < 0) {
             const uint4 o = philox10(t_lo, t_hi, 0u, STREAM_START | qs, a.k0, a.k1);
             rx_start = (int)(o.x % (uint32_t)(a.wave_len - L));
         }
-        float2 *r = rbase + (rx_start & 3);             // r[n] = capture sample n
-        if (a.ext && first_item) {
-            for (int n = tid; n < L; n += SYNC_THREADS) r[n] = a.ext[n];
+        const int off = rx_start & 3;
+        const float *r = rbase + off;                       // r[n] = Re capture sample n
+        // Im capture sample n = imt[im0 + n] reduced mod the period (a.im_period: nfilt, or 2^30 for ext)
+        const int im0 = ext ? 0 : rx_start % a.im_period;
+        if (ext) {
+            for (int n = lane; n < L; n += 64) rbase[off + n] = a.ext[n].x;
         } else {
             const int b0 = rx_start >> 2, b1 = (rx_start + L - 1) >> 2;
-            const PhiloxHead hd = philox_head(t_lo, t_hi, STREAM_NOISE | qs, a.k1);   // shared by all blocks
+            const PhiloxHead hd = philox_head(t_lo, t_hi, STREAM_NOISE | qs, a.k1);
             const float Ksig = noise_k(sigma);
-            // Gaussian k of the trial's stream goes to waveform sample k (as if Transmission_Over_Air
-            // had drawn the whole waveform); only the captured samples are ever evaluated.
-            // FRAME_CAP_U Philox blocks per lane per pass, their waveform loads issued first.
-#ifndef FRAME_CAP_U
-#define FRAME_CAP_U 3   // Philox blocks per lane per pass: 752-block captures in 2 full passes (A/B: +1.7 % over 4)
-#endif
-            // The waveform is FR_REPS copies of one filtered frame (OFDM.c:607-612): sample k is sample
-            // k mod nfilt of the first copy, so every trial reads the same 7.8 KB (L1-resident) instead of
-            // its own 24 KB window of the 78 KB waveform.  bm = the block's index within the copy
-            // (nfilt is a multiple of 4; pb > SYNC_THREADS, so one conditional subtract per step).
+            // Gaussian k of the trial's stream goes to waveform sample k (as if Transmission_Over_Air had drawn
+            // the whole waveform); only the captured samples are ever evaluated.  The waveform is FR_REPS
+            // copies of one filtered frame (OFDM.c:607-612): sample k is sample k mod nfilt of the first copy
+            // (7.8 KB, L1-resident).  bm = the block's index within the copy.
             const uint32_t pb = (uint32_t)(a.wave_len / (4 * FR_REPS)), nb_wave = (uint32_t)(a.wave_len / 4);
-            uint32_t bm = (uint32_t)(b0 + tid) % pb;
-            for (int bb = b0 + tid; bb <= b1; bb += FRAME_CAP_U * SYNC_THREADS) {
-                float2 v[FRAME_CAP_U][4];
+            uint32_t bm = (uint32_t)(b0 + lane) % pb;
+#ifndef FRAME_CAP_U
+#define FRAME_CAP_U 3
+#endif
+            for (int bb = b0 + lane; bb <= b1; bb += FRAME_CAP_U * 64) {
+                float4 v[FRAME_CAP_U];
 #pragma unroll
                 for (int u = 0; u < FRAME_CAP_U; ++u) {
-                    const int b = bb + SYNC_THREADS * u;
-#ifdef OFDM_FRAME_WAVE_FULL     // A/B: read the full 78 KB waveform
-                    const float4 *s4 = reinterpret_cast<const float4 *>(a.wave + 4 * b);
-#else
+                    const int b = bb + 64 * u;
                     const float4 *s4 = reinterpret_cast<const float4 *>(a.wave + 4 * bm);
-#endif
                     const bool in = b <= b1 && (uint32_t)b < nb_wave;
                     const float4 lo = in ? s4[0] : make_float4(0.f, 0.f, 0.f, 0.f);
                     const float4 hi = in ? s4[1] : make_float4(0.f, 0.f, 0.f, 0.f);
-                    v[u][0] = make_float2(lo.x, lo.y); v[u][1] = make_float2(lo.z, lo.w);
-                    v[u][2] = make_float2(hi.x, hi.y); v[u][3] = make_float2(hi.z, hi.w);
-                    bm = min(bm + SYNC_THREADS, bm + SYNC_THREADS - pb);     // (bm + 128) mod pb, unsigned
+                    v[u] = make_float4(lo.x, lo.z, hi.x, hi.z);
+                    bm = bm + 64 >= pb ? bm + 64 - pb : bm + 64;           // (bm + 64) mod pb (pb > 64)
                 }
-#ifdef OFDM_FRAME_CAP_VKEYS   // A/B: the pass's Philox blocks together, round keys in VGPRs
-                uint4 po[FRAME_CAP_U];
-                if (a.noise == OFDM_NOISE_REAL) {
-                    uint32_t c2s[FRAME_CAP_U];
-#pragma unroll
-                    for (int u = 0; u < FRAME_CAP_U; ++u) c2s[u] = (uint32_t)(bb + SYNC_THREADS * u);
-                    philox10_c2_vk<FRAME_CAP_U>(hd, c2s, a.k0, a.k1, po);
-                }
-#endif
 #pragma unroll
                 for (int u = 0; u < FRAME_CAP_U; ++u) {
-                    const int b = bb + SYNC_THREADS * u;
+                    const int b = bb + 64 * u;
                     if (b > b1) break;
-                    float2 w[4];
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) w[j] = v[u][j];
+                    float4 w = v[u];
                     if (a.noise == OFDM_NOISE_REAL) {   // real-only (D7): sigma z = sqrt(K log2 u1) (cos | sin)
-#ifdef OFDM_FRAME_CAP_VKEYS
-                        const Noise4 nz = noise4_of(po[u], Ksig);
-#else
                         const Noise4 nz = noise4_of(philox10_c2(hd, (uint32_t)b, a.k0, a.k1), Ksig);
-#endif
-                        w[0].x = fmaf(nz.r0, nz.c0, w[0].x); w[1].x = fmaf(nz.r0, nz.s0, w[1].x);
-                        w[2].x = fmaf(nz.r1, nz.c1, w[2].x); w[3].x = fmaf(nz.r1, nz.s1, w[3].x);
+                        w.x = fmaf(nz.r0, nz.c0, w.x); w.y = fmaf(nz.r0, nz.s0, w.y);
+                        w.z = fmaf(nz.r1, nz.c1, w.z); w.w = fmaf(nz.r1, nz.s1, w.w);
                     }
                     // samples of the block outside [0, L) land in the region's slack, never read as capture
-                    float4 *d4 = reinterpret_cast<float4 *>(rbase + 4 * (b - b0));
-                    d4[0] = make_float4(w[0].x, w[0].y, w[1].x, w[1].y);
-                    d4[1] = make_float4(w[2].x, w[2].y, w[3].x, w[3].y);
+                    *reinterpret_cast<float4 *>(rbase + 4 * (b - b0)) = w;
                 }
             }
         }
-        for (int k = tid; k < cross_words(L); k += SYNC_THREADS) cross[k] = 0ull;
-        __syncthreads();
-#ifndef OFDM_FRAME_STATIC_ITEMS
-        if (i + 1 < run_end) {
-            inext = i + 1;
-        } else {
-            inext = (int64_t)__builtin_amdgcn_readfirstlane(redi[RED_I_NEXT]) * FRAME_ITEM_RUN;
-            run_end = inext + FRAME_ITEM_RUN;
-        }
-#else
-        inext = i + gridDim.x;
-#endif
+        wave_lds_sync();
         FR_STAMP(0);                                           // capture + noise
+        // lane-derived values are re-derived per item, not held across the item loop
+        int lx = lane;
+        opaque(lx);
 
-        // ---- Word_Optimization_Analysis(Rx_filter_signal) (OFDM.c:38-73, 962-967): the full RRC
-        // matched filter of the capture, min / max over real and imaginary parts (opt-in) ----
+        // ---- Word_Optimization_Analysis(Rx_filter_signal) (OFDM.c:38-73, 962-967): the full RRC matched
+        // filter of the capture, min / max over real and imaginary parts (opt-in) ----
         if (a.word_stats) {
             float mn = 1e9f, mx = -1e9f;
-            for (int k = tid; k < L + 20; k += SYNC_THREADS) {
+            for (int k = lx; k < L + 20; k += 64) {
                 float2 v = make_float2(0.f, 0.f);
 #pragma unroll
                 for (int j = 0; j < 21; ++j) {
                     const int m = k - j;
                     if (m >= 0 && m < L) {
-                        v.x = fmaf(r[m].x, a.taps[j], v.x);
-                        v.y = fmaf(r[m].y, a.taps[j], v.y);
+                        const int mi = (im0 + m) % a.im_period;
+                        v.x = fmaf(r[m], a.taps[j], v.x);
+                        v.y = fmaf(imt[mi], a.taps[j], v.y);
                     }
                 }
                 mn = fminf(mn, fminf(v.x, v.y));
@@ -548,293 +516,222 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
             }
             mn = wave_min_f(mn);
             mx = wave_max_f(mx);
-            __syncthreads();
-            if (lane == 0) { redf[2 * (tid >> 6)] = mn; redf[2 * (tid >> 6) + 1] = mx; }
-            __syncthreads();
-            if (tid == 0) {
-                float bmn = redf[0], bmx = redf[1];
-                for (int w = 1; w < SYNC_WAVES; ++w) { bmn = fminf(bmn, redf[2 * w]); bmx = fmaxf(bmx, redf[2 * w + 1]); }
-                unsigned long long *sl = acc + q * ACC_SLOTS;
-                sl[10] = (unsigned long long)min((long long)sl[10], (long long)__float2ll_rn(bmn * (float)OFDM_EVM_Q_SCALE));
-                sl[11] = (unsigned long long)max((long long)sl[11], (long long)__float2ll_rn(bmx * (float)OFDM_EVM_Q_SCALE));
+            if (lx == 0) {
+                atomicMin(reinterpret_cast<long long *>(&acc[q * ns + 2]), (long long)__float2ll_rn(mn * (float)OFDM_EVM_Q_SCALE));
+                atomicMax(reinterpret_cast<long long *>(&acc[q * ns + 3]), (long long)__float2ll_rn(mx * (float)OFDM_EVM_Q_SCALE));
             }
         }
 
         // ---- Packet_Detection (OFDM.c:659-683): M[n] = |sum r[n+k] r[n+k+16]|^2 / (sum |r[n+k+16]|^2)^2,
-        // k < 32, no conjugate, on the UNFILTERED capture; sliding sums over each lane's chunk with the
-        // LDS reads issued DET_B positions at a time.  M > 0.75 (OFDM.c:687, 695) is decided as the sign
-        // of t = 0.75 den - num (fma: exact before its one rounding): t < 0 <=> crossing, which keeps the
-        // division's outcomes 0/0 -> false (t = +0) and x/0 -> true (t = -num). ----
-        const int n0 = tid * chunk, n1 = min(n0 + chunk, Lc);
-        unsigned long long cmask = 0ull;            // crossing n at bit n - n0 (chunk <= 64)
-#ifndef FRAME_DET_B
-#define FRAME_DET_B 5
-#endif
-        constexpr int DET_B = FRAME_DET_B;
-        if (n0 < n1) {
-#ifdef OFDM_FRAME_DET_OLD      // A/B: products formed, then added (9 VALU per window term, 24 per position)
-            float sx = 0.f, sy = 0.f, pw = 0.f;
+        // k < 32, no conjugate, on the UNFILTERED capture; sliding sums over each lane's chunk with the LDS
+        // reads issued DET_B positions at a time.  M > 0.75 (OFDM.c:687, 695) is decided as the sign of
+        // t = 0.75 den - num (fma: exact before its one rounding): t < 0 <=> crossing, which keeps the
+        // division's outcomes 0/0 -> false (t = +0) and x/0 -> true (t = -num).  Lane l of round rho owns
+        // positions [(64 rho + l) chunk, +chunk); crossing n at bit n - n0 of the round's mask. ----
+        unsigned long long cm[2] = {0ull, 0ull};
+        int first[2] = {-1, -1}, last[2] = {-1, -1};
+        static_for<0, 2>([&](auto rc) {
+            constexpr int rho = decltype(rc)::value;
+            const int n0 = (64 * rho + lx) * chunk, n1 = min(n0 + chunk, Lc);
+            unsigned long long cmask = 0ull;
+            if (rho < R && n0 < n1) {
+                const float *ti_ = imt + (im0 + n0) % a.im_period;   // Im of sample n0 + k at ti_[k] (k < IMT_EXT)
+                const float *tr_ = r + n0;
+                float sx = 0.f, sy = 0.f, pw = 0.f;
 #pragma unroll 8
-            for (int k = 0; k < 32; ++k) {
-                const float2 u = r[n0 + k], v = r[n0 + k + 16];
-                sx += u.x * v.x - u.y * v.y;
-                sy += u.x * v.y + u.y * v.x;
-                pw += v.x * v.x + v.y * v.y;
-            }
-            for (int nb = n0; nb < n1; nb += DET_B) {
-                float2 o0[DET_B], o1[DET_B], i0[DET_B], i1[DET_B];
-#pragma unroll
-                for (int k = 0; k < DET_B; ++k) {
-                    o0[k] = r[nb + k]; o1[k] = r[nb + k + 16]; i0[k] = r[nb + k + 32]; i1[k] = r[nb + k + 48];
+                for (int k = 0; k < 32; ++k) {
+                    const float ux = tr_[k], uy = ti_[k], vx = tr_[k + 16], vy = ti_[k + 16];
+                    sx = fmaf(ux, vx, sx); sx = fmaf(-uy, vy, sx);
+                    sy = fmaf(ux, vy, sy); sy = fmaf(uy, vx, sy);
+                    pw = fmaf(vx, vx, pw); pw = fmaf(vy, vy, pw);
                 }
-                uint32_t m = 0u;
+                // t's sign bits shifted in with v_alignbit, one per position (first position highest); every
+                // active lane runs the same ceil(chunk / DET_B) batches, positions past n1 are masked below
+                uint32_t mlo = 0u, mhi = 0u;
+                const int nbat = (chunk + DET_B - 1) / DET_B;
+                for (int b = 0; b < nbat; ++b) {
+                    const int nb = DET_B * b;
+                    float o0x[DET_B], o0y[DET_B], o1x[DET_B], o1y[DET_B], i0x[DET_B], i0y[DET_B], i1x[DET_B], i1y[DET_B];
 #pragma unroll
-                for (int k = 0; k < DET_B; ++k) {
-                    const float num = sx * sx + sy * sy, den = pw * pw;
-                    m |= num > 0.75f * den ? 1u << k : 0u;
-                    sx += (i0[k].x * i1[k].x - i0[k].y * i1[k].y) - (o0[k].x * o1[k].x - o0[k].y * o1[k].y);
-                    sy += (i0[k].x * i1[k].y + i0[k].y * i1[k].x) - (o0[k].x * o1[k].y + o0[k].y * o1[k].x);
-                    pw += (i1[k].x * i1[k].x + i1[k].y * i1[k].y) - (o1[k].x * o1[k].x + o1[k].y * o1[k].y);
-                }
-                cmask |= (unsigned long long)m << (nb - n0);
-            }
-#else
-            // every window term accumulated by fma straight into the running sums (6 VALU per term; the
-            // sliding update is 12 fma per position: the entering product added, the leaving one taken off)
-            float sx = 0.f, sy = 0.f, pw = 0.f;
-#pragma unroll 8
-            for (int k = 0; k < 32; ++k) {
-                const float2 u = r[n0 + k], v = r[n0 + k + 16];
-                sx = fmaf(u.x, v.x, sx); sx = fmaf(-u.y, v.y, sx);
-                sy = fmaf(u.x, v.y, sy); sy = fmaf(u.y, v.x, sy);
-                pw = fmaf(v.x, v.x, pw); pw = fmaf(v.y, v.y, pw);
-            }
-            // t's sign bits shifted in with v_alignbit, one per position (first position highest); every
-            // active lane runs the same ceil(chunk / DET_B) batches, positions past n1 are masked below
-            uint32_t mlo = 0u, mhi = 0u;
-            const int nbat = (chunk + DET_B - 1) / DET_B;
-            for (int b = 0; b < nbat; ++b) {
-                const int nb = n0 + DET_B * b;
-                float2 o0[DET_B], o1[DET_B], i0[DET_B], i1[DET_B];
+                    for (int k = 0; k < DET_B; ++k) {   // reads past the capture land in the region's slack
+                        o0x[k] = tr_[nb + k]; o1x[k] = tr_[nb + k + 16]; i0x[k] = tr_[nb + k + 32]; i1x[k] = tr_[nb + k + 48];
+                        o0y[k] = ti_[nb + k]; o1y[k] = ti_[nb + k + 16]; i0y[k] = ti_[nb + k + 32]; i1y[k] = ti_[nb + k + 48];
+                    }
 #pragma unroll
-                for (int k = 0; k < DET_B; ++k) {       // reads past the capture land in the region's slack / cross
-                    o0[k] = r[nb + k]; o1[k] = r[nb + k + 16]; i0[k] = r[nb + k + 32]; i1[k] = r[nb + k + 48];
+                    for (int k = 0; k < DET_B; ++k) {
+                        const float num = fmaf(sx, sx, sy * sy), h = 0.75f * pw;
+                        const float tt = fmaf(h, pw, -num);
+                        mhi = __builtin_amdgcn_alignbit(mhi, mlo, 31);
+                        mlo = __builtin_amdgcn_alignbit(mlo, __float_as_uint(tt), 31);
+                        sx = fmaf(i0x[k], i1x[k], sx); sx = fmaf(-i0y[k], i1y[k], sx);
+                        sx = fmaf(-o0x[k], o1x[k], sx); sx = fmaf(o0y[k], o1y[k], sx);
+                        sy = fmaf(i0x[k], i1y[k], sy); sy = fmaf(i0y[k], i1x[k], sy);
+                        sy = fmaf(-o0x[k], o1y[k], sy); sy = fmaf(-o0y[k], o1x[k], sy);
+                        pw = fmaf(i1x[k], i1x[k], pw); pw = fmaf(i1y[k], i1y[k], pw);
+                        pw = fmaf(-o1x[k], o1x[k], pw); pw = fmaf(-o1y[k], o1y[k], pw);
+                    }
                 }
-#pragma unroll
-                for (int k = 0; k < DET_B; ++k) {
-                    const float num = fmaf(sx, sx, sy * sy), h = 0.75f * pw;
-                    const float t = fmaf(h, pw, -num);
-                    if (chunk > 32) mhi = __builtin_amdgcn_alignbit(mhi, mlo, 31);
-                    mlo = __builtin_amdgcn_alignbit(mlo, __float_as_uint(t), 31);
-                    sx = fmaf(i0[k].x, i1[k].x, sx); sx = fmaf(-i0[k].y, i1[k].y, sx);
-                    sx = fmaf(-o0[k].x, o1[k].x, sx); sx = fmaf(o0[k].y, o1[k].y, sx);
-                    sy = fmaf(i0[k].x, i1[k].y, sy); sy = fmaf(i0[k].y, i1[k].x, sy);
-                    sy = fmaf(-o0[k].x, o1[k].y, sy); sy = fmaf(-o0[k].y, o1[k].x, sy);
-                    pw = fmaf(i1[k].x, i1[k].x, pw); pw = fmaf(i1[k].y, i1[k].y, pw);
-                    pw = fmaf(-o1[k].x, o1[k].x, pw); pw = fmaf(-o1[k].y, o1[k].y, pw);
-                }
+                // J = nbat * DET_B <= 64 positions: position j sits at bit J - 1 - j of (mhi:mlo); reverse
+                const int J = nbat * DET_B;
+                const unsigned long long rev = ((unsigned long long)__builtin_bitreverse32(mlo) << 32) |
+                                               __builtin_bitreverse32(mhi);
+                cmask = rev >> (64 - J);
+                cmask &= (1ull << (n1 - n0)) - 1ull;          // the last batch's positions past n1 (n1 - n0 < 64)
             }
-            // J = nbat * DET_B positions: position j sits at bit J - 1 - j of (mhi:mlo); reverse the bits
-            const int J = nbat * DET_B;
-            const unsigned long long rev = ((unsigned long long)__builtin_bitreverse32(mlo) << 32) |
-                                           __builtin_bitreverse32(mhi);
-            cmask = rev >> (64 - J);
-#endif
-            if (n1 - n0 < 64) cmask &= (1ull << (n1 - n0)) - 1ull;   // the last batch's positions past n1
-            if (cmask) {
-                atomicOr(&cross[n0 >> 6], cmask << (n0 & 63));
-                if ((n0 & 63) + chunk > 64) atomicOr(&cross[(n0 >> 6) + 1], cmask >> (64 - (n0 & 63)));
-            }
-        }
-        // first / last crossing in this lane's chunk
-        const int first = cmask ? n0 + __builtin_ctzll(cmask) : -1;
-        const int last = cmask ? n0 + 63 - __builtin_clzll(cmask) : -1;
+            cm[rho] = cmask;
+            first[rho] = cmask ? n0 + __builtin_ctzll(cmask) : -1;
+            last[rho] = cmask ? n0 + 63 - __builtin_clzll(cmask) : -1;
+        });
         if (a.dbg_corr && first_item) {             // Corr_Out for ofdm_receiver's parity dump
-            for (int n = tid; n < Lc; n += SYNC_THREADS) {
+            for (int n = lx; n < Lc; n += 64) {
                 float sx = 0.f, sy = 0.f, pw = 0.f;
                 for (int k = 0; k < 32; ++k) {
-                    const float2 u = r[n + k], v = r[n + k + 16];
-                    sx += u.x * v.x - u.y * v.y;
-                    sy += u.x * v.y + u.y * v.x;
-                    pw += v.x * v.x + v.y * v.y;
+                    const float ux = r[n + k], uy = imt[(im0 + n + k) % a.im_period];
+                    const float vx = r[n + k + 16], vy = imt[(im0 + n + k + 16) % a.im_period];
+                    sx += ux * vx - uy * vy;
+                    sy += ux * vy + uy * vx;
+                    pw += vx * vx + vy * vy;
                 }
                 a.dbg_corr[n] = (sx * sx + sy * sy) / (pw * pw);
             }
         }
+        FR_STAMP(1);                                           // packet detection
 
         // ---- Packet_Selection (OFDM.c:685-771): crossing idx[j] is a front iff idx[j] - idx[j-1] > 300
-        // (idx[-1] = -1).  Fronts are > 300 apart and a chunk is < 300 positions, so only a lane's
-        // first crossing can be one, and its predecessor is the last crossing of the earlier chunks:
-        // an exclusive prefix max over the block's lanes.  The first front x with a later front and
-        // M[front+230] > 0.75 gives packet_idx = front + len_RRC_rx + 1; otherwise 0 (OFDM.c:752-761). ----
-#ifdef OFDM_FRAME_SCAN_SHFL     // A/B: the ds_bpermute ladder
-        int pm = last;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int t2 = __shfl_up(pm, o, 64);
-            if (lane >= o) pm = max(pm, t2);
-        }
-        int prev = __shfl_up(pm, 1, 64);
-        if (lane == 0) prev = -1;
-#else
-        const int pm = wave_prefix_max(last);
-        int prev = wave_shr1(pm);
-#endif
-        if (lane == 63) redi[RED_I_PREFIX + (tid >> 6)] = pm;   // each wave's last crossing
-        __syncthreads();                            // crossing words and wave prefixes are in LDS
-        for (int w = 0; w < (tid >> 6); ++w) prev = max(prev, redi[RED_I_PREFIX + w]);   // earlier waves
-        const int front = (first >= 0 && first - prev > 300) ? first : -1;
-        FR_STAMP(1);                                           // packet detection
-        const bool valid = front >= 0 && front + 230 < Lc && bit_at(cross, front + 230);
+        // (idx[-1] = -1).  Fronts are > 300 apart and a chunk is < 300 positions, so only a lane's first
+        // crossing can be one, and its predecessor is the last crossing of the earlier chunks: an exclusive
+        // prefix max over (round, lane).  The first front x with a later front and M[front+230] > 0.75 gives
+        // packet_idx = front + len_RRC_rx + 1; otherwise 0 (OFDM.c:752-761). ----
+        int vmin = 0x7fffffff, fmax_ = -1, carry = -1;
+        static_for<0, 2>([&](auto rc) {
+            constexpr int rho = decltype(rc)::value;
+            if (rho < R) {
+                const int pm = max(wave_prefix_max(last[rho]), carry);
+                const int prev = max(wave_shr1(pm), carry);
+                const int front = (first[rho] >= 0 && first[rho] - prev > 300) ? first[rho] : -1;
+                carry = __builtin_amdgcn_readlane(pm, 63);
+                // the crossing bit of position front + 230 from the lane that owns it (ds_bpermute)
+                const int pos = front + 230;
+                const int v = pos / chunk, owner = v & 63, bit = pos - v * chunk;
+                unsigned long long w = 0ull;
+                static_for<0, 2>([&](auto r2c) {
+                    constexpr int r2 = decltype(r2c)::value;
+                    if (r2 < R) {
+                        const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)cm[r2], owner, 64);
+                        const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(cm[r2] >> 32), owner, 64);
+                        if ((v >> 6) == r2) w = ((unsigned long long)hi << 32) | lo;
+                    }
+                });
+                const bool valid = front >= 0 && pos < Lc && ((w >> bit) & 1ull);
+                vmin = min(vmin, valid ? front : 0x7fffffff);
+                fmax_ = max(fmax_, front);
+            }
+        });
         // the first valid front that has a later front: the least valid front, unless it is the last one
-#ifdef OFDM_FRAME_MINMAX_LEAD   // A/B: the leading barrier kept
-        const int2 mm = block_minmax_i<true>(valid ? front : 0x7fffffff, front, redi + RED_I_MINMAX);
-#else
-        const int2 mm = block_minmax_i<false>(valid ? front : 0x7fffffff, front, redi + RED_I_MINMAX);
-#endif
-        const int cand = mm.x < mm.y ? mm.x : 0x7fffffff;
+        const int cmin = wave_min_i(vmin), cmax = wave_max_i(fmax_);
+        const int cand = cmin < cmax ? cmin : 0x7fffffff;
         const bool sync_fail = cand == 0x7fffffff;
         const int p = sync_fail ? 0 : cand + 10 + 1;           // len_RRC_rx + 1 (OFDM.c:758)
         FR_STAMP(2);                                           // packet selection
 
-        // fr[] in the unread prefix [0, off + lo) or suffix (off + hi, region) of the capture region
+        // fr[] (float2) in the unread prefix [0, off + lo) or the unread suffix (off + hi, region) of the region
+        float2 *fr = fr_sep;
         if (a.fr_in_cap) {
-            const int off = rx_start & 3, lo = max(p - 20, 0), hi = min(p + 2 * nfr - 2, L - 1);
-            fr = off + lo >= nfr ? rbase : rbase + off + hi + 1;
+            const int lo = max(p - 20, 0), hi = min(p + 2 * nfr - 2, L - 1);
+            fr = off + lo >= 2 * nfr ? reinterpret_cast<float2 *>(rbase)
+                                     : reinterpret_cast<float2 *>(rbase + ((off + hi + 2) & ~1));
         }
         // ---- RRC matched filter at the down-sampled instants p + 2i (OFDM.c:965, 992-996): outputs
-        // interleaved over the lanes, so a tap's reads are 2 samples apart across lanes; clamped reads +
-        // select are Convolution's zero padding.  Only the 160 + 64 nd frame samples the receiver reads
-        // are filtered (needed_k: the coarse-CFO STF lag window, both LTFs, the data windows without
-        // their CPs), all nfr for the single-capture dump.  The OOB flag is unchanged: the reference
+        // interleaved over the lanes, so a tap's reads are 2 samples apart across lanes (ds_read_b64 pairs:
+        // adjacent lanes read adjacent 8 B).  Only the 160 + 64 nd frame samples the receiver reads are
+        // filtered (needed_k), all nfr for the single-capture dump.  The OOB flag is unchanged: the reference
         // reads past its buffer iff the last instant does, and the last sample is always needed. ----
         const bool dbg = a.dbg_frame && first_item;
         bool oob_l = false;
-        // taps copied to VGPRs: an FMA with an SGPR operand issues in the slow class (+0.6 %)
         float tv[21];
-#ifdef FRAME_TAPS_SGPR
-#pragma unroll
-        for (int j = 0; j < 21; ++j) tv[j] = a.taps[j];
-#else
         {
-            // read from the kernarg segment through a pointer made opaque per item, so the 21 taps are
-            // scalar-loaded here and die at the copy instead of being hoisted into SGPRs held across the
-            // item loop (they were most of the loop's SGPR spills)
+            // taps scalar-loaded from the kernarg segment per item and moved to VGPRs (an FMA with an SGPR
+            // operand issues in the slow class), dying after the filter
             using kchar = __attribute__((address_space(4))) char;
             using kfloat = __attribute__((address_space(4))) float;
             const kfloat *tp = (const kfloat *)((const kchar *)__builtin_amdgcn_kernarg_segment_ptr() +
-                                                    offsetof(FrameArgs, taps));
+                                                offsetof(FrameArgs, taps));
             asm volatile("" : "+s"(tp));
 #pragma unroll
             for (int j = 0; j < 21; ++j) asm volatile("v_mov_b32 %0, %1" : "=v"(tv[j]) : "s"(tp[j]));
         }
-#endif
-#ifdef OFDM_FRAME_MF_ALL      // A/B: filter every frame sample
-        const int nmf = nfr;
-#else
         const int nmf = dbg ? nfr : 160 + 64 * a.n_data;
-#endif
-        for (int j = tid; j < nmf; j += SYNC_THREADS) {
-#ifdef OFDM_FRAME_MF_ALL
-            const int ii = j;
-#else
+        // parities of the first float of a filter window in the region and in the table: uniform per item
+        // (n = p + 2 ii; the period is even)
+        const int par_r = (off + p) & 1, par_i = (im0 + p) & 1;
+        for (int j = lx; j < nmf; j += 64) {
             const int ii = dbg ? j : needed_k(j);
-#endif
             const int n = p + 2 * ii;
             float2 v = make_float2(0.f, 0.f);
             if (n >= 20 && n < L) {                              // all 21 taps inside the capture
-#ifdef OFDM_FRAME_MF_B64      // A/B: one ds_read_b64 per tap (lanes 16 B apart: 2-way bank conflicts)
-                float2 x[21];
+                float xr[21], xi[21];                            // x[t] = sample n - t
+                const int si = (im0 + n - 20) % a.im_period;
+                if (par_r) lds_read21<1>(rbase, off + n - 20, xr); else lds_read21<0>(rbase, off + n - 20, xr);
+                if (par_i) lds_read21<1>(imt, si, xi); else lds_read21<0>(imt, si, xi);
 #pragma unroll
-                for (int t = 0; t < 21; ++t) x[t] = r[n - t];
-#else
-                // samples n-20 .. n as 10 sample pairs + 1 single: a ds_read_b128 per pair, 16-byte
-                // aligned in the region (rbase); lanes read adjacent 16 B (conflict-free).  The pairs start
-                // at n-20 or n-19 depending on the parity of the region index, uniform per item.
-                float2 x[21];                                    // x[t] = sample n - t
-                const int s0 = n - 20 + (rx_start & 3);          // region index of sample n - 20
-                auto load = [&](auto oc) {
-                    constexpr int ODD = decltype(oc)::value;
-                    const float4 *q4 = reinterpret_cast<const float4 *>(rbase + s0 + ODD);
-#pragma unroll
-                    for (int m = 0; m < 10; ++m) {
-                        const float4 w = q4[m];                  // samples n-20+ODD+2m, n-19+ODD+2m
-                        x[20 - ODD - 2 * m] = make_float2(w.x, w.y);
-                        x[19 - ODD - 2 * m] = make_float2(w.z, w.w);
-                    }
-                    x[ODD ? 20 : 0] = rbase[ODD ? s0 : s0 + 20];  // the sample the pairs leave out
-                };
-                if (s0 & 1) load(std::integral_constant<int, 1>{});
-                else load(std::integral_constant<int, 0>{});
-#endif
-#pragma unroll
-                for (int t = 0; t < 21; ++t) {
-                    v.x = fmaf(x[t].x, tv[t], v.x);
-                    v.y = fmaf(x[t].y, tv[t], v.y);
+                for (int tt = 0; tt < 21; ++tt) {
+                    v.x = fmaf(xr[tt], tv[tt], v.x);
+                    v.y = fmaf(xi[tt], tv[tt], v.y);
                 }
             } else if (n >= L + 20) {
                 oob_l = true;                                    // the reference reads past its buffer
             } else {
 #pragma unroll
-                for (int t = 0; t < 21; ++t) {
-                    const int m = n - t;
-                    float2 x = r[min(max(m, 0), L - 1)];
-                    x = (m >= 0 && m < L) ? x : make_float2(0.f, 0.f);
-                    v.x = fmaf(x.x, tv[t], v.x);
-                    v.y = fmaf(x.y, tv[t], v.y);
+                for (int tt = 0; tt < 21; ++tt) {
+                    const int m = n - tt;
+                    const int mc = min(max(m, 0), L - 1);
+                    const bool in = m >= 0 && m < L;
+                    const float xr = in ? r[mc] : 0.f, xi = in ? imt[(im0 + mc) % a.im_period] : 0.f;
+                    v.x = fmaf(xr, tv[tt], v.x);
+                    v.y = fmaf(xi, tv[tt], v.y);
                 }
             }
             fr[ii] = v;                                          // outside every lane's reads
         }
-        // each wave's OOB flag, read by thread 0 after the barrier that also orders fr[] for every lane
-        if (lane == 0) redi[RED_I_MAX + (tid >> 6)] = __ballot(oob_l) != 0ull;
-        __syncthreads();
+        const bool oob = __ballot(oob_l) != 0ull;
+        wave_lds_sync();
         FR_STAMP(3);                                           // matched filter + down-sample
 
         // ---- Coarse CFO (OFDM.c:773-804): 16-lag autocorrelation of the short preamble; fine CFO
         // (OFDM.c:806-828): 64-lag over the two long training symbols after the coarse rotation, the 128
         // rotated LTF samples formed on the fly (the same arithmetic as rotating the whole frame first).
-        // Wave 0 holds every term: both estimates are wave reductions there, and one barrier hands the
-        // frequencies to the other waves. ----
-        double *cfo_sh = reinterpret_cast<double *>(redf);      // [fc, ff]
-        if (tid < 64) {
-            float2 pp = make_float2(0.f, 0.f);
-            if (tid < 16) {
-                const float2 u = fr[80 + tid], v = fr[96 + tid];
-                pp = make_float2(u.x * v.x + u.y * v.y, u.y * v.x - u.x * v.y);
-            }
-            pp.x = wave_sum_f(pp.x);
-            pp.y = wave_sum_f(pp.y);
-            double fc = (-1.0 / (2.0 * M_PI * 16.0 * TS)) * (double)atan2f(pp.y, pp.x);
-            if (a.float_cfo) fc = (double)(float)fc;
-            const float2 u = cfo_rot(fr[192 + tid], fc * TS, 192 + tid), v = cfo_rot(fr[256 + tid], fc * TS, 256 + tid);
-            pp = make_float2(u.x * v.x + u.y * v.y, u.y * v.x - u.x * v.y);
-            pp.x = wave_sum_f(pp.x);
-            pp.y = wave_sum_f(pp.y);
-            double ff = (-1.0 / (2.0 * M_PI * 64.0 * TS)) * (double)atan2f(pp.y, pp.x);
-            if (a.float_cfo) ff = (double)(float)ff;
-            if (tid == 0) { cfo_sh[0] = fc; cfo_sh[1] = ff; }
+        // Both estimates are wave reductions. ----
+        float2 pp = make_float2(0.f, 0.f);
+        if (lx < 16) {
+            const float2 u = fr[80 + lx], w = fr[96 + lx];
+            pp = make_float2(u.x * w.x + u.y * w.y, u.y * w.x - u.x * w.y);
         }
-        __syncthreads();
-        const double fc = cfo_sh[0], ff = cfo_sh[1];
-        (void)fc; (void)ff;
+        pp.x = wave_sum_f(pp.x);
+        pp.y = wave_sum_f(pp.y);
+        double fc = (-1.0 / (2.0 * M_PI * 16.0 * TS)) * (double)atan2f(pp.y, pp.x);
+        if (a.float_cfo) fc = (double)(float)fc;
+        {
+            const float2 u = cfo_rot(fr[192 + lx], fc * TS, 192 + lx), w = cfo_rot(fr[256 + lx], fc * TS, 256 + lx);
+            pp = make_float2(u.x * w.x + u.y * w.y, u.y * w.x - u.x * w.y);
+        }
+        pp.x = wave_sum_f(pp.x);
+        pp.y = wave_sum_f(pp.y);
+        double ff = (-1.0 / (2.0 * M_PI * 64.0 * TS)) * (double)atan2f(pp.y, pp.x);
+        if (a.float_cfo) ff = (double)(float)ff;
         // ---- coarse then fine rotation (OFDM.c:802, 825) as ONE rotation by the summed phase
-        // 2 pi (fc + ff) Ts k, evaluated in fp64 revolutions (the reference's two double-precision
-        // cexp products rounded to float twice; the same rotation to fp32 rounding), the result handed
-        // off directly: LTF1 [192,256), LTF2 [256,320), data d [336 + 80 d, +64) (OFDM.c:830-850,
-        // 1024-1040) ----
+        // 2 pi (fc + ff) Ts k, evaluated in fp64 revolutions (the reference's two double-precision cexp
+        // products rounded to float twice; the same rotation to fp32 rounding), the result handed off
+        // directly: LTF1 [192,256), LTF2 [256,320), data d [336 + 80 d, +64) (OFDM.c:830-850, 1024-1040) ----
         const int nw = 2 + a.n_data;
         float2 *dst = win_item(a.win, a.ipb, nw, i);
         const int row = a.ipb * nw;                            // float2 between samples n and n + 1
-#ifndef OFDM_FRAME_CFO_TWO_STEP
         const double fcf_ts = (fc + ff) * TS;
-#endif
-        // hand-off element j = sample j / nw of window j % nw: consecutive lanes fill the item's nw
-        // adjacent slots of a tile row (j / nw by a 16-bit reciprocal, exact for j < 64 nw <= 640);
-        // the dump rotates all nfr samples
+        // hand-off element j = sample j / nw of window j % nw: consecutive lanes fill the item's nw adjacent
+        // slots of a tile row (j / nw by a 16-bit reciprocal, exact for j < 64 nw <= 640); the dump rotates
+        // all nfr samples
         const int nrot = dbg ? nfr : 64 * nw;
         const uint32_t inv_nw = (65536u + (uint32_t)nw - 1u) / (uint32_t)nw;
-        for (int j = tid; j < nrot; j += SYNC_THREADS) {
+        for (int j = lx; j < nrot; j += 64) {
             int n = (int)(((uint32_t)j * inv_nw) >> 16), w = j - n * nw;
             int k = needed_k(64 * w + n + 32);
             if (dbg) {
@@ -846,42 +743,42 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINB) void frame_sync_kern
                     if (d < a.n_data && o < 64) { w = 2 + d; n = o; }
                 }
             }
-#ifdef OFDM_FRAME_CFO_TWO_STEP
-            const float2 v = cfo_rot(cfo_rot(fr[k], fc * TS, k), ff * TS, k);
-#else
             const float2 v = cfo_rot(fr[k], fcf_ts, k);
-#endif
             if (dbg) a.dbg_frame[k] = v;
             if (w >= 0) dst[n * row + w] = v;
         }
         FR_STAMP(4);                                           // coarse + fine CFO + hand-off
-        if (tid == 0) {
-            int oob = 0;
-#pragma unroll
-            for (int w = 0; w < SYNC_WAVES; ++w) oob |= redi[RED_I_MAX + w];
+        if (lx == 0) {
             a.info[i] = make_int4(p, sync_fail, oob, rx_start);
-            unsigned long long *sl = acc + q * ACC_SLOTS;
-            sl[3] += sync_fail;
-            sl[4] += oob;
+            if (sync_fail) atomicAdd(&acc[q * ns + 0], 1ull);
+            if (oob) atomicAdd(&acc[q * ns + 1], 1ull);
             if (a.pidx_out) a.pidx_out[(int64_t)q * a.n_trials + ti] = p;
             if (first_item && a.dbg_ints) { a.dbg_ints[0] = p; a.dbg_ints[1] = sync_fail; a.dbg_ints[2] = oob; a.dbg_ints[3] = rx_start; }
         }
-        __syncthreads();
+        // the next item: the next one of this run, or the first of the run fetched at this run's start
+        if (i + 1 < run_end) {
+            ++i;
+        } else {
+            i = (int64_t)__builtin_amdgcn_readfirstlane(nxt) * FRAME_ITEM_RUN;
+            run_end = i + FRAME_ITEM_RUN;
+        }
+        // the next capture overwrites this item's region: every lane is done reading it
+        wave_lds_sync();
         FR_STAMP(6);                                           // hand-off
     }
 #ifdef OFDM_FRAME_STAMPS
-    if (threadIdx.x == 0 && a.stamps)
+    if (lane == 0 && a.stamps)
         for (int k = 0; k < 7; ++k) atomicAdd(&a.stamps[k], stamp_acc[k]);
 #endif
     __syncthreads();
-    for (int k = tid; k < a.n_snr; k += SYNC_THREADS) {
+    for (int k = threadIdx.x; k < a.n_snr; k += SYNC_THREADS) {
         unsigned long long *c = a.counters + k * OFDM_NCOUNTERS;
-        const unsigned long long *sl = acc + k * ACC_SLOTS;
-        if (sl[3]) atomicAdd(&c[OFDM_C_SYNC_FAIL], sl[3]);
-        if (sl[4]) atomicAdd(&c[OFDM_C_OOB], sl[4]);
+        const unsigned long long *sl = acc + k * ns;
+        if (sl[0]) atomicAdd(&c[OFDM_C_SYNC_FAIL], sl[0]);
+        if (sl[1]) atomicAdd(&c[OFDM_C_OOB], sl[1]);
         if (a.word_stats) {
-            atomicMin(reinterpret_cast<long long *>(&c[OFDM_C_WL_MIN_Q]), (long long)sl[10]);
-            atomicMax(reinterpret_cast<long long *>(&c[OFDM_C_WL_MAX_Q]), (long long)sl[11]);
+            atomicMin(reinterpret_cast<long long *>(&c[OFDM_C_WL_MIN_Q]), (long long)sl[2]);
+            atomicMax(reinterpret_cast<long long *>(&c[OFDM_C_WL_MAX_Q]), (long long)sl[3]);
         }
     }
 }
@@ -1108,22 +1005,20 @@ static int run_frame_chunk(Ctx *c, FrameArgs &a) {
     if (rc) return rc;
     a.win = (float2 *)c->d_scratch;
     a.info = (int4 *)((char *)c->d_scratch + ((wbytes + 255) & ~size_t(255)));
-    const size_t lds = frame_lds_bytes(a.cap_len, a.n_data, a.n_snr);
-#ifdef OFDM_FR_SEPARATE
-    a.fr_in_cap = 0;
-#else
+    // the capture's imaginary parts: one waveform copy (+ IMT_EXT) for generated captures, the external
+    // capture's own for ofdm_receiver
+    a.im_period = a.ext ? (1 << 30) : a.wave_len / FR_REPS;
+    a.imt_len = (a.ext ? a.cap_len : a.im_period) + IMT_EXT;
+    const size_t lds = frame_lds_bytes(a.cap_len, a.n_data, a.n_snr, a.imt_len, a.word_stats);
     a.fr_in_cap = fr_in_capture(a.cap_len, a.n_data);
-#endif
     if (!c->d_work) HIPOK(hipMalloc(&c->d_work, 256));
     a.work = (unsigned long long *)c->d_work;
     HIPOK(hipMemsetAsync(c->d_work, 0, sizeof(unsigned long long), c->stream));
-#ifndef OFDM_FRAME_SYNC_WAVES
-#define OFDM_FRAME_SYNC_WAVES 2
-#endif
-    const int sync_waves = OFDM_FRAME_SYNC_WAVES;
+    // one resident grid: every wave starts with a run of items, the rest come from the work counter
+    const int64_t runs = (a.n_items + FRAME_ITEM_RUN - 1) / FRAME_ITEM_RUN;
     hipLaunchKernelGGL(frame_sync_kernel,
                        dim3(occupancy_grid(reinterpret_cast<const void *>(&frame_sync_kernel), SYNC_THREADS, lds,
-                                           c->cus, a.n_items, sync_waves)),
+                                           c->cus, (runs + SYNC_WAVES - 1) / SYNC_WAVES, 1)),
                        dim3(SYNC_THREADS), lds, c->stream, a);
     const int ipb = (SYM_THREADS / 4) / ((a.n_data + 1) / 2);
     const bool dump = a.dbg_eq || a.dbg_bits || a.dbg_res;
