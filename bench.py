@@ -125,8 +125,9 @@ def make_roofline(pmc: dict, lib_id: str | None, kernel: str, workload: str, uni
     cap = issue_cap(pmc, frac) if model and model.get("build_id") == lib_id else {}
     return {**base, "achieved": achieved, "frac": frac, "instr_per_unit": ipu,
             "pmc_source": "profiles/pmc_summary.json[%s]" % {"c4": "c3"}.get(workload, workload),
-            **({"fused_tx": "the receiver launches of chunks 0..n-2 also build the next chunk's Tx batch "
-                            "(ofdm_set_next_tx); their VALU and HBM counts include it"} if fused_tx else {}),
+            **({"fused_tx": "the receivers build the step's Tx batches: chunk 0's its own (ofdm_txrx_frames), "
+                            "chunk k's the batch of chunk k+1 (ofdm_set_next_tx); their VALU and HBM counts include "
+                            "it"} if fused_tx else {}),
             **cap}, traffic
 
 
@@ -283,12 +284,13 @@ def plan_chunks(first: int, frames: int) -> list[tuple[int, int]]:
 
 
 class PipelinedSymbolStep:
-    """One symbol-mode step: Tx + receiver of every chunk into two alternating Tx batches.  `fused`: the
-    receiver of chunk k builds chunk k+1's batch in its group prologues (ofdm_set_next_tx; the packed LS
-    receivers run it on the waves that idle while the clean spectra are transformed), one stream.  Otherwise
-    the Tx of chunk k+1 runs on a second stream while the receiver of chunk k runs (tools/overlap_ab.py:
-    c3 +1.5-2.7 %, counters bit-identical); events order each batch's reuse after the receiver that read it,
-    and a step's Tx stream after every receiver of the previous step."""
+    """One symbol-mode step: Tx + receiver of every chunk into two alternating Tx batches.  `fused` (the packed
+    real-noise receivers): the receivers build every batch, one stream -- chunk 0's receiver its own batch
+    (ofdm_txrx_frames: each group's symbols built in its prologue, then read back) and the receiver of chunk k
+    chunk k+1's batch (ofdm_set_next_tx, on the waves that idle while the clean spectra are transformed).
+    Otherwise the Tx of chunk k+1 runs on a second stream while the receiver of chunk k runs
+    (tools/overlap_ab.py: c3 +1.5-2.7 %, counters bit-identical); events order each batch's reuse after the
+    receiver that read it, and a step's Tx stream after every receiver of the previous step."""
 
     def __init__(self, torch, eng, cfg, chunks, counters, dev: int, fused: bool = False):
         self.torch, self.eng, self.cfg, self.chunks, self.counters = torch, eng, cfg, chunks, counters
@@ -302,14 +304,15 @@ class PipelinedSymbolStep:
         s_rx, s_tx = self.s_rx, self.s_tx
         self.counters.zero_()
         if self.fused:
-            # the packed LS receiver of chunk k builds chunk k+1's Tx batch on its blocks' idle prologue
-            # waves (ofdm_set_next_tx); one stream: the batch it overwrites was last read by receiver k-1
+            # one stream: the batch receiver k overwrites (chunk k+1's) was last read by receiver k-1
             eng.set_stream(s_rx.cuda_stream)
-            eng.tx_frames(cfg, chunks[0][0], chunks[0][1], *bufs[0])
             for k, (a, n) in enumerate(chunks):
                 if k + 1 < len(chunks):
                     eng.set_next_tx(cfg, chunks[k + 1][0], chunks[k + 1][1], *bufs[(k + 1) % 2])
-                eng.rx_frames(cfg, *bufs[k % 2], a, n, SNR_GRID, self.counters)
+                if k == 0:
+                    eng.txrx_frames(cfg, a, n, SNR_GRID, *bufs[0], self.counters)
+                else:
+                    eng.rx_frames(cfg, *bufs[k % 2], a, n, SNR_GRID, self.counters)
             return
         tx_done = [torch.cuda.Event() for _ in chunks]
         rx_done = [torch.cuda.Event() for _ in chunks]
@@ -383,9 +386,9 @@ def main():
     frame_mode = args.workload == "frame"
     counters = eng.new_counters(len(SNR_GRID))
     chunks = plan_chunks(first, frames)
-    # LS sweeps on real noise (c3, c4, c5): the next chunk's Tx fused into the receiver's group prologues;
-    # c2 (ideal CSI): the Tx of chunk k+1 on a second stream
-    fused = (kw.get("est") == "ls" and kw.get("noise") == "real") if args.pipeline == "auto" else args.pipeline == "fused"
+    # real-noise sweeps on the packed receivers (c2, c3, c4, c5): every Tx batch built inside the receivers
+    packed = kw.get("noise") == "real" and (kw.get("channel") == "awgn" or kw.get("est") == "ls")
+    fused = packed if args.pipeline == "auto" else args.pipeline == "fused"
     sym_step = (PipelinedSymbolStep(torch, eng, cfg, chunks, counters, dev, fused=fused)
                 if not frame_mode and chunks else None)
 
@@ -441,7 +444,7 @@ def main():
               else ("rx_ls_kernel" if kw.get("est") == "ls" else "rx_ideal_kernel"))
     lib_id = codeobj.workload_build_id(abi.library_file(), args.workload)
     roofline, traffic = make_roofline(pmc, lib_id, kernel, args.workload, units_per_launch, rx_avg_s, rx_n,
-                                      fused and len(chunks) > 1)
+                                      fused and not frame_mode)
     hbm_alg = units_per_launch * bytes_per_unit / rx_avg_s / 1e9
     if rank == 0:
         line = {

@@ -50,6 +50,7 @@ _SIGS = {
     "ofdm_tx_frames": (C.c_int, [_V, _V, C.c_uint64, C.c_int64, _V, _V]),
     "ofdm_set_next_tx": (C.c_int, [_V, _V, C.c_uint64, C.c_int64, _V, _V]),
     "ofdm_rx_frames": (C.c_int, [_V, _V, _V, _V, C.c_uint64, C.c_int64, _V, C.c_int, _V]),
+    "ofdm_txrx_frames": (C.c_int, [_V, _V, C.c_uint64, C.c_int64, _V, _V, _V, C.c_int, _V]),
     "ofdm_rx_frames_dump": (C.c_int, [_V, _V, _V, _V, C.c_uint64, C.c_int64, _V, C.c_int, _V, _V, _V]),
     "ofdm_symbol_sweep": (C.c_int, [_V, _V, _V, C.c_int, C.c_uint64, C.c_int64, C.c_int64, _V]),
     "ofdm_set_message": (C.c_int, [_V, C.c_char_p, C.c_int32, C.POINTER(C.c_int32)]),

@@ -18,7 +18,7 @@ CSRC = PKG_DIR / "csrc"
 INCLUDE = PKG_DIR.parent / "include"
 BUILD = PKG_DIR / "_build"
 LIB = PKG_DIR / "libofdm_mi355x.so"
-SOURCES = ["ofdm_capi.hip", "ofdm_symbol.hip", "ofdm_rxpack.hip", "ofdm_frame.hip"]
+SOURCES = ["ofdm_capi.hip", "ofdm_symbol.hip", "ofdm_rxpack.hip", "ofdm_rxpack_ideal.hip", "ofdm_frame.hip"]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -fno-slp-vectorize: keep f32 math scalar (packed v_pk_* f32 gives no rate on gfx950 and its
@@ -30,9 +30,11 @@ CFLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-fno-slp-vecto
 
 # per-source flags: the symbol-mode kernels schedule for ILP (A/B: c3 +1 %, c2 +3 %, c5 +3 %; the
 # frame kernels -0.5 %, profiles/r01/ab/ab_*_ilp.json; packed receivers c3 +1.4 %, c2 +2.5 %,
-# profiles/r02/ab/SUMMARY.md)
+# profiles/r02/ab/SUMMARY.md).  The packed ideal-CSI receivers (ofdm_rxpack_ideal.hip) keep the default scheduler:
+# with the prologue's Tx builds, max-ILP spills them at their 168-VGPR budget.
 SOURCE_FLAGS = {"ofdm_symbol.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
-                "ofdm_rxpack.hip": os.environ.get("OFDM_RXPACK_FLAGS", "-mllvm -amdgpu-sched-strategy=max-ilp").split()}
+                "ofdm_rxpack.hip": os.environ.get("OFDM_RXPACK_FLAGS", "-mllvm -amdgpu-sched-strategy=max-ilp").split(),
+                "ofdm_rxpack_ideal.hip": os.environ.get("OFDM_RXPACK_IDEAL_FLAGS", "").split()}
 
 
 # Kernels whose parity-dump variants (last template argument `true`) are allowed to spill: they

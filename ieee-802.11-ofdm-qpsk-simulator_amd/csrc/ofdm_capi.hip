@@ -342,8 +342,10 @@ int ofdm_set_next_tx(ofdm_ctx *ctx, const ofdm_cfg *cfg, uint64_t first_frame, i
     return OFDM_OK;
 }
 
+// own_tx: the call also builds the batch it reads (ofdm_txrx_frames), d_tx / d_bits then being writable
 static int rx_common(Ctx *c, const ofdm_cfg *cfg, const void *d_tx, const void *d_bits, uint64_t first_frame,
-                     int64_t n_frames, const double *snr_db, int n_snr, void *d_counters, void *d_eq, void *d_dbits) {
+                     int64_t n_frames, const double *snr_db, int n_snr, void *d_counters, void *d_eq, void *d_dbits,
+                     bool own_tx = false) {
     if (!c) return set_error(OFDM_E_ARG, "ctx is NULL");
     // every argument check first: a call that fails them returns with a pending ofdm_set_next_tx batch still
     // pending (nothing consumed, nothing launched)
@@ -358,14 +360,22 @@ static int rx_common(Ctx *c, const ofdm_cfg *cfg, const void *d_tx, const void *
     // launches it, otherwise built by the Tx kernel right here (same stream, so it is ready in either case
     // once this call's work is)
     bool fuse_nx = false;
+    const bool packed = !dump && n_frames > 0 && n_snr > 0 && rx_pack_applies(*cfg);
     if (c->nx_pending) {
         c->nx_pending = false;
-        fuse_nx = !dump && n_frames > 0 && n_snr > 0 && rx_pack_applies(*cfg) && cfg->est == OFDM_EST_LS;
+        fuse_nx = packed;
         if (!fuse_nx) {
             const int rt = ofdm_tx_frames(reinterpret_cast<ofdm_ctx *>(c), &c->nx_cfg, c->nx_first, c->nx_n,
                                           c->nx_tx, c->nx_bits);
             if (rt) return rt;
         }
+    }
+    // the call's own batch: built in the packed receiver's group prologues, otherwise by the Tx kernel first
+    const bool fuse_own = own_tx && packed;
+    if (own_tx && !fuse_own) {
+        const int rt = ofdm_tx_frames(reinterpret_cast<ofdm_ctx *>(c), cfg, first_frame, n_frames,
+                                      const_cast<void *>(d_tx), const_cast<void *>(d_bits));
+        if (rt) return rt;
     }
     if (n_frames == 0 || n_snr == 0) return OFDM_OK;
     HIPOK(hipSetDevice(c->device));
@@ -401,6 +411,10 @@ static int rx_common(Ctx *c, const ofdm_cfg *cfg, const void *d_tx, const void *
             a.nx = tx_args(c, &c->nx_cfg, c->nx_first, c->nx_n, c->nx_tx, c->nx_bits);
             a.nx_conv = c->nx_cfg.conv;
         }
+        if (fuse_own && q0 == 0) {       // later SNR slices read the batch the first launch built
+            a.own = tx_args(c, cfg, first_frame, n_frames, const_cast<void *>(d_tx), const_cast<void *>(d_bits));
+            a.own_conv = cfg->conv;
+        }
         if (!c->d_work) HIPOK(hipMalloc(&c->d_work, 256));
         a.work = (unsigned long long *)c->d_work;
         HIPOK(hipMemsetAsync(c->d_work, 0, sizeof(unsigned long long), c->stream));
@@ -435,6 +449,14 @@ int ofdm_rx_frames_dump(ofdm_ctx *ctx, const ofdm_cfg *cfg, const void *d_tx, co
                         void *d_eq, void *d_dbits) {
     return rx_common(reinterpret_cast<Ctx *>(ctx), cfg, d_tx, d_bits, first_frame, n_frames, snr_db, n_snr,
                      d_counters, d_eq, d_dbits);
+}
+
+int ofdm_txrx_frames(ofdm_ctx *ctx, const ofdm_cfg *cfg, uint64_t first_frame, int64_t n_frames, void *d_tx,
+                     void *d_bits, const double *snr_db, int n_snr, void *d_counters) {
+    Ctx *c = reinterpret_cast<Ctx *>(ctx);
+    int rc = check_tx(c, cfg, n_frames, d_tx, d_bits);
+    if (rc) return rc;
+    return rx_common(c, cfg, d_tx, d_bits, first_frame, n_frames, snr_db, n_snr, d_counters, nullptr, nullptr, true);
 }
 
 int ofdm_symbol_sweep(ofdm_ctx *ctx, const ofdm_cfg *cfg, const double *snr_db, int n_snr, uint64_t first_frame,
@@ -483,10 +505,10 @@ int ofdm_symbol_sweep(ofdm_ctx *ctx, const ofdm_cfg *cfg, const double *snr_db, 
     auto chunk_of = [&](int64_t k, int64_t *first, int64_t *nf) { *first = first_frame + k * cf; *nf = std::min(cf, n_frames - k * cf); };
     int64_t f0, n0;
     chunk_of(0, &f0, &n0);
-    if ((rc = ofdm_tx_frames(ctx, cfg, f0, n0, txbuf[0], bitbuf[0]))) return rc;
-    if (n_chunks > 1 && rx_pack_applies(*cfg) && cfg->est == OFDM_EST_LS) {
-        // the packed LS receiver of chunk k builds chunk k+1's batch in its group prologues (ofdm_set_next_tx),
-        // one stream: the batch it overwrites was last read by receiver k-1
+    if (rx_pack_applies(*cfg)) {
+        // the packed receivers build the Tx batches themselves, one stream: chunk 0's receiver its own batch
+        // (ofdm_txrx_frames) and the receiver of chunk k chunk k+1's batch (ofdm_set_next_tx) in their group
+        // prologues; the batch a receiver overwrites was last read by receiver k-1
         for (int64_t k = 0; k < n_chunks; ++k) {
             if (k + 1 < n_chunks) {
                 int64_t f1, n1;
@@ -495,12 +517,15 @@ int ofdm_symbol_sweep(ofdm_ctx *ctx, const ofdm_cfg *cfg, const double *snr_db, 
             }
             int64_t fk, nk;
             chunk_of(k, &fk, &nk);
-            if ((rc = ofdm_rx_frames(ctx, cfg, txbuf[k & 1], bitbuf[k & 1], fk, nk, snr_db, n_snr, c->d_cnt))) return rc;
+            rc = k == 0 ? ofdm_txrx_frames(ctx, cfg, fk, nk, txbuf[0], bitbuf[0], snr_db, n_snr, c->d_cnt)
+                        : ofdm_rx_frames(ctx, cfg, txbuf[k & 1], bitbuf[k & 1], fk, nk, snr_db, n_snr, c->d_cnt);
+            if (rc) return rc;
         }
         HIPOK(hipMemcpyAsync(counters, c->d_cnt, cbytes, hipMemcpyDeviceToHost, c->stream));
         HIPOK(hipStreamSynchronize(c->stream));
         return OFDM_OK;
     }
+    if ((rc = ofdm_tx_frames(ctx, cfg, f0, n0, txbuf[0], bitbuf[0]))) return rc;
     for (int64_t k = 0; k < n_chunks; ++k) {
         if (k + 1 < n_chunks) {                                  // Tx of chunk k+1 into the other batch
             if (k >= 1) HIPOK(hipStreamWaitEvent(c->tx_stream, c->ev_rx[(k - 1) & 1], 0));   // chunk k-1 read it

@@ -59,6 +59,7 @@ struct FrameArgs {
     int32_t cap_len, float_cfo, matlab, fixed_start, noise, wave_len, n_data, word_stats;
     int32_t fr_in_cap;              // fr[] inside the capture region (fr_in_capture)
     int32_t imt_len, im_period;     // LDS table of the capture's imaginary parts: length, index period
+    uint32_t im_magic;              // ceil(2^32 / im_period): x mod im_period by one multiply-high (x < 2^14)
     uint32_t k0, k1;
     uint32_t table[3 * FR_MAX_DATA];
     uint32_t dtable[4 * FR_MAX_DATA];   // demap words of the payload symbols (ofdm_rxcommon.h)
@@ -362,6 +363,13 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// x mod the table period for 0 <= x < 2^14 (q = floor(x / period) by multiply-high: exact there)
+template <typename A>
+__device__ __forceinline__ int im_mod(const A &a, int x) {
+    const uint32_t q = __umulhi((uint32_t)x, a.im_magic);
+    return x - (int)(q * (uint32_t)a.im_period);
+}
+
 // 21 contiguous LDS floats p[s .. s + 20] into x[20 - t] = p[s + t] order reversed (x[t] = sample n - t for
 // s = n - 20), as 10 ds_read_b64 + 1 ds_read_b32; ODD = s & 1 (uniform per item: the pairs are 8-byte aligned)
 template <int ODD>
@@ -444,16 +452,23 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
             const uint4 o = philox10(t_lo, t_hi, 0u, STREAM_START | qs, a.k0, a.k1);
             rx_start = (int)(o.x % (uint32_t)(a.wave_len - L));
         }
+        rx_start = __builtin_amdgcn_readfirstlane(rx_start);     // uniform: the capture geometry in SGPRs
         const int off = rx_start & 3;
         const float *r = rbase + off;                       // r[n] = Re capture sample n
         // Im capture sample n = imt[im0 + n] reduced mod the period (a.im_period: nfilt, or 2^30 for ext)
-        const int im0 = ext ? 0 : rx_start % a.im_period;
+        const int im0 = ext ? 0 : im_mod(a, rx_start);
         if (ext) {
             for (int n = lane; n < L; n += 64) rbase[off + n] = a.ext[n].x;
         } else {
             const int b0 = rx_start >> 2, b1 = (rx_start + L - 1) >> 2;
             const PhiloxHead hd = philox_head(t_lo, t_hi, STREAM_NOISE | qs, a.k1);
             const float Ksig = noise_k(sigma);
+#ifndef FRAME_CAP_SKEYS
+            // round keys in VGPRs: each round's two v_bitop3_b32 issue at the fast rate (an SGPR operand makes
+            // them slow-class); 20 VGPRs for the capture loop only
+            PhiloxKeysV vk;
+            vk.init(a.k0, a.k1);
+#endif
             // Gaussian k of the trial's stream goes to waveform sample k (as if Transmission_Over_Air had drawn
             // the whole waveform); only the captured samples are ever evaluated.  The waveform is FR_REPS
             // copies of one filtered frame (OFDM.c:607-612): sample k is sample k mod nfilt of the first copy
@@ -481,7 +496,11 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
                     if (b > b1) break;
                     float4 w = v[u];
                     if (a.noise == OFDM_NOISE_REAL) {   // real-only (D7): sigma z = sqrt(K log2 u1) (cos | sin)
+#ifndef FRAME_CAP_SKEYS
+                        const Noise4 nz = noise4_of(philox10_c2(hd, (uint32_t)b, vk), Ksig);
+#else
                         const Noise4 nz = noise4_of(philox10_c2(hd, (uint32_t)b, a.k0, a.k1), Ksig);
+#endif
                         w.x = fmaf(nz.r0, nz.c0, w.x); w.y = fmaf(nz.r0, nz.s0, w.y);
                         w.z = fmaf(nz.r1, nz.c1, w.z); w.w = fmaf(nz.r1, nz.s1, w.w);
                     }
@@ -506,7 +525,7 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
                 for (int j = 0; j < 21; ++j) {
                     const int m = k - j;
                     if (m >= 0 && m < L) {
-                        const int mi = (im0 + m) % a.im_period;
+                        const int mi = im_mod(a, im0 + m);
                         v.x = fmaf(r[m], a.taps[j], v.x);
                         v.y = fmaf(imt[mi], a.taps[j], v.y);
                     }
@@ -535,7 +554,7 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
             const int n0 = (64 * rho + lx) * chunk, n1 = min(n0 + chunk, Lc);
             unsigned long long cmask = 0ull;
             if (rho < R && n0 < n1) {
-                const float *ti_ = imt + (im0 + n0) % a.im_period;   // Im of sample n0 + k at ti_[k] (k < IMT_EXT)
+                const float *ti_ = imt + im_mod(a, im0 + n0);   // Im of sample n0 + k at ti_[k] (k < IMT_EXT)
                 const float *tr_ = r + n0;
                 float sx = 0.f, sy = 0.f, pw = 0.f;
 #pragma unroll 8
@@ -586,8 +605,8 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
             for (int n = lx; n < Lc; n += 64) {
                 float sx = 0.f, sy = 0.f, pw = 0.f;
                 for (int k = 0; k < 32; ++k) {
-                    const float ux = r[n + k], uy = imt[(im0 + n + k) % a.im_period];
-                    const float vx = r[n + k + 16], vy = imt[(im0 + n + k + 16) % a.im_period];
+                    const float ux = r[n + k], uy = imt[im_mod(a, im0 + n + k)];
+                    const float vx = r[n + k + 16], vy = imt[im_mod(a, im0 + n + k + 16)];
                     sx += ux * vx - uy * vy;
                     sy += ux * vy + uy * vx;
                     pw += vx * vx + vy * vy;
@@ -648,7 +667,9 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
         // reads past its buffer iff the last instant does, and the last sample is always needed. ----
         const bool dbg = a.dbg_frame && first_item;
         bool oob_l = false;
-        float tv[21];
+        // the RRC taps are symmetric (h[t] = h[20 - t], OFDM.c:32; rrc_taps), so a window is 10 pair sums + the
+        // centre tap: 11 FMAs per component instead of 21
+        float tv[11];
         {
             // taps scalar-loaded from the kernarg segment per item and moved to VGPRs (an FMA with an SGPR
             // operand issues in the slow class), dying after the filter
@@ -658,7 +679,7 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
                                                 offsetof(FrameArgs, taps));
             asm volatile("" : "+s"(tp));
 #pragma unroll
-            for (int j = 0; j < 21; ++j) asm volatile("v_mov_b32 %0, %1" : "=v"(tv[j]) : "s"(tp[j]));
+            for (int j = 0; j < 11; ++j) asm volatile("v_mov_b32 %0, %1" : "=v"(tv[j]) : "s"(tp[j]));
         }
         const int nmf = dbg ? nfr : 160 + 64 * a.n_data;
         // parities of the first float of a filter window in the region and in the table: uniform per item
@@ -670,13 +691,14 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
             float2 v = make_float2(0.f, 0.f);
             if (n >= 20 && n < L) {                              // all 21 taps inside the capture
                 float xr[21], xi[21];                            // x[t] = sample n - t
-                const int si = (im0 + n - 20) % a.im_period;
+                const int si = im_mod(a, im0 + n - 20);
                 if (par_r) lds_read21<1>(rbase, off + n - 20, xr); else lds_read21<0>(rbase, off + n - 20, xr);
                 if (par_i) lds_read21<1>(imt, si, xi); else lds_read21<0>(imt, si, xi);
+                v = make_float2(xr[10] * tv[10], xi[10] * tv[10]);
 #pragma unroll
-                for (int tt = 0; tt < 21; ++tt) {
-                    v.x = fmaf(xr[tt], tv[tt], v.x);
-                    v.y = fmaf(xi[tt], tv[tt], v.y);
+                for (int tt = 0; tt < 10; ++tt) {
+                    v.x = fmaf(xr[tt] + xr[20 - tt], tv[tt], v.x);
+                    v.y = fmaf(xi[tt] + xi[20 - tt], tv[tt], v.y);
                 }
             } else if (n >= L + 20) {
                 oob_l = true;                                    // the reference reads past its buffer
@@ -686,9 +708,10 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
                     const int m = n - tt;
                     const int mc = min(max(m, 0), L - 1);
                     const bool in = m >= 0 && m < L;
-                    const float xr = in ? r[mc] : 0.f, xi = in ? imt[(im0 + mc) % a.im_period] : 0.f;
-                    v.x = fmaf(xr, tv[tt], v.x);
-                    v.y = fmaf(xi, tv[tt], v.y);
+                    const float xr = in ? r[mc] : 0.f, xi = in ? imt[im_mod(a, im0 + mc)] : 0.f;
+                    const float h = tv[tt <= 10 ? tt : 20 - tt];
+                    v.x = fmaf(xr, h, v.x);
+                    v.y = fmaf(xi, h, v.y);
                 }
             }
             fr[ii] = v;                                          // outside every lane's reads
@@ -915,6 +938,7 @@ static void rrc_taps(float out[21]) {
         e += b * b;
     }
     for (int i = 0; i < 21; ++i) out[i] = (float)(h[i] / std::sqrt(e));
+    for (int i = 0; i < 10; ++i) out[20 - i] = out[i];      // symmetric (the sync kernel folds the taps)
 }
 
 }  // namespace ofdm
@@ -1008,6 +1032,7 @@ static int run_frame_chunk(Ctx *c, FrameArgs &a) {
     // the capture's imaginary parts: one waveform copy (+ IMT_EXT) for generated captures, the external
     // capture's own for ofdm_receiver
     a.im_period = a.ext ? (1 << 30) : a.wave_len / FR_REPS;
+    a.im_magic = (uint32_t)((((uint64_t)1 << 32) + (uint64_t)a.im_period - 1) / (uint64_t)a.im_period);
     a.imt_len = (a.ext ? a.cap_len : a.im_period) + IMT_EXT;
     const size_t lds = frame_lds_bytes(a.cap_len, a.n_data, a.n_snr, a.imt_len, a.word_stats);
     a.fr_in_cap = fr_in_capture(a.cap_len, a.n_data);

@@ -58,6 +58,8 @@ struct RxArgs {
     unsigned long long *work;          // K3c: work items handed out past the first gridDim.x (zeroed per launch)
     TxArgs nx;                         // K3c: the NEXT chunk's Tx batch, built in the group prologues (n_sym 0: none)
     int32_t nx_conv;                   // its ifft convention
+    TxArgs own;                        // K3c: THIS launch's Tx batch (ofdm_txrx_frames), each group built by the
+    int32_t own_conv;                  // items that read it, before its clean spectra (n_sym 0: none)
     float sigma[OFDM_MAX_SNR];
 };
 
@@ -69,5 +71,8 @@ int rx_grid(const ofdm_cfg &cfg, int64_t n_frames, int device);
 bool rx_pack_applies(const ofdm_cfg &cfg);
 void launch_rx_pack(hipStream_t st, const RxArgs &a, const ofdm_cfg &cfg, bool dump, unsigned grid);
 int rx_pack_grid(const ofdm_cfg &cfg, int64_t n_frames, int device);
+// K3c's ideal-CSI instantiations (ofdm_rxpack_ideal.hip)
+void launch_rx_pack_ideal(hipStream_t st, const RxArgs &a, const ofdm_cfg &cfg, bool dump, unsigned grid);
+int rx_pack_ideal_grid(int64_t n_frames, int device);
 
 }  // namespace ofdm

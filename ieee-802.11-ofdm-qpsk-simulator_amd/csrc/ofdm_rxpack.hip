@@ -236,6 +236,26 @@ __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_
         // loop (they would be the only values spilled)
         int t = tid;
         opaque(t);
+        // kernel arguments read where used through an opaque kernarg pointer: hoisted, the 40 words of each
+        // TxArgs would be held in SGPRs across the item loop and spill
+        using KArgs = const __attribute__((address_space(4))) RxArgs;
+        KArgs *ap = (KArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(ap));
+        const bool own_tx = ap->own.n_sym > 0;
+        if (own_tx) {
+            // this launch's own batch (ofdm_txrx_frames): waves 2-3 build the group's 128 symbols (K2's code,
+            // byte-identical), and after the barrier the block reads them back from its XCD's L2 like a batch
+            // built by an earlier launch.  Every item of a group builds it (a tail group's SNR subsets run on
+            // several blocks): the duplicate stores write identical bytes.
+            if (t >= PK_SYMS) {
+                const int64_t sidx = grp * PK_SYMS + (t - PK_SYMS);
+                if (sidx < ap->own.n_sym) {
+                    if (ap->own_conv == OFDM_CONV_C) tx_symbol<OFDM_CONV_C>(ap->own, sidx);
+                    else tx_symbol<OFDM_CONV_MATLAB>(ap->own, sidx);
+                }
+            }
+            __syncthreads();
+        }
 #ifdef OFDM_ABL_NO_PREPASS
         if (t < PK_SYMS && grp == blockIdx.x) {
 #else
@@ -252,15 +272,16 @@ __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_
 #ifndef OFDM_PACK_STATIC_ITEMS
                 int nx = 0;
                 if (j == 0) nx = B + (int)atomicAdd(a.work, 1ull);
-                nx = __builtin_amdgcn_readfirstlane(__shfl(nx, 0, 64));
+                nx = __builtin_amdgcn_readlane(nx, 0);          // lane 0 (j == 0) fetched it
 #else
                 const int nx = w + B;
 #endif
                 if (j == 0) next_item = nx;
 #ifndef OFDM_PACK_NO_L2_WARM
                 // warm L2 with the next item's group (64 rows x 1 KB: one 4-byte LDS-DMA read per 128-B
-                // line, into a dummy LDS word), so the next prologue's loads hit L2 instead of HBM
-                if (nx < n_items) {
+                // line, into a dummy LDS word), so the next prologue's loads hit L2 instead of HBM (not when
+                // the launch builds its own batch: those rows are written by the next item itself)
+                if (nx < n_items && !own_tx) {
                     const int64_t ng = nx < R * B ? nx : R * B + (nx - R * B) / S;
 #pragma unroll
                     for (int i = 0; i < 8; ++i) {
@@ -274,12 +295,7 @@ __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_
             }
             // the next chunk's Tx batch (ofdm_set_next_tx), one symbol per lane: group gg of this launch's
             // sub-0 item builds the next batch's symbols [128 gg', 128 gg' + 128) for gg' = gg, gg + G, ...
-            // (its arguments are re-read through an opaque kernarg pointer: hoisted, the 40 words of TxArgs
-            // would be held in SGPRs across the item loop and spill)
-            using KArgs = const __attribute__((address_space(4))) RxArgs;
-            KArgs *ap = (KArgs *)__builtin_amdgcn_kernarg_segment_ptr();
-            asm volatile("" : "+s"(ap));
-            if (KIND == 2 && ap->nx.n_sym > 0 && sub == 0) {     // LS receivers (the chunked benchmarks)
+            if (ap->nx.n_sym > 0 && sub == 0) {
                 for (int64_t sidx = grp * PK_SYMS + j; sidx < ap->nx.n_sym; sidx += (int64_t)G * PK_SYMS) {
                     if (ap->nx_conv == OFDM_CONV_C) tx_symbol<OFDM_CONV_C>(ap->nx, sidx);
                     else tx_symbol<OFDM_CONV_MATLAB>(ap->nx, sidx);
@@ -509,6 +525,30 @@ static void launch_pack_t(hipStream_t st, const RxArgs &a, bool dump, unsigned g
     else hipLaunchKernelGGL((rx_pack_kernel<KIND, CONV, CHAN, false>), dim3(grid), dim3(256), 0, st, a);
 }
 
+template <const void *(*K)()>
+static int pack_grid(int64_t n_frames, int device) {
+    const int64_t need = (n_frames + PK_FRAMES - 1) / PK_FRAMES;
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, K(), 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1) cus = 256;
+    const int64_t cap = (int64_t)per_cu * cus;
+    const int64_t g = need < cap ? need : cap;
+    return (int)(g < 1 ? 1 : g);
+}
+
+#ifdef OFDM_RXPACK_IDEAL_TU
+// The ideal-CSI receivers (KIND 0) are instantiated in their own translation unit (ofdm_rxpack_ideal.hip),
+// compiled with LLVM's default scheduler: with the group prologue's Tx builds, max-ILP scheduling of the
+// 168-VGPR (3 waves/SIMD) receiver spills, the default one fits (163 VGPRs).
+static const void *ideal_kernel() { return reinterpret_cast<const void *>(&rx_pack_kernel<0, OFDM_CONV_C, OFDM_CHAN_AWGN, false>); }
+
+void launch_rx_pack_ideal(hipStream_t st, const RxArgs &a, const ofdm_cfg &cfg, bool dump, unsigned grid) {
+    if (cfg.conv == OFDM_CONV_C) launch_pack_t<0, OFDM_CONV_C>(st, a, dump, grid);
+    else launch_pack_t<0, OFDM_CONV_MATLAB>(st, a, dump, grid);
+}
+
+int rx_pack_ideal_grid(int64_t n_frames, int device) { return pack_grid<ideal_kernel>(n_frames, device); }
+#else
 // Real-noise sweeps: AWGN with either estimator, and the 4-tap Rayleigh channel with the LS estimator
 // (the ideal-CSI Rayleigh ZF and every complex-noise sweep run the {E, D0, D1} / ideal receivers).
 bool rx_pack_applies(const ofdm_cfg &cfg) {
@@ -528,22 +568,19 @@ void launch_rx_pack(hipStream_t st, const RxArgs &a, const ofdm_cfg &cfg, bool d
     if (cfg.est == OFDM_EST_LS && cfg.channel == OFDM_CHAN_RAYLEIGH4)
         launch_pack_t<2, OFDM_CONV_C, OFDM_CHAN_RAYLEIGH4>(st, a, dump, grid);           // conv via a.ltf
     else if (cfg.est == OFDM_EST_LS) launch_pack_t<2, OFDM_CONV_C>(st, a, dump, grid);
-    else if (cfg.conv == OFDM_CONV_C) launch_pack_t<0, OFDM_CONV_C>(st, a, dump, grid);
-    else launch_pack_t<0, OFDM_CONV_MATLAB>(st, a, dump, grid);
+    else launch_rx_pack_ideal(st, a, cfg, dump, grid);
+}
+
+static const void *ls_kernel() { return reinterpret_cast<const void *>(&rx_pack_kernel<2, OFDM_CONV_C, OFDM_CHAN_AWGN, false>); }
+static const void *fade_kernel() {
+    return reinterpret_cast<const void *>(&rx_pack_kernel<2, OFDM_CONV_C, OFDM_CHAN_RAYLEIGH4, false>);
 }
 
 int rx_pack_grid(const ofdm_cfg &cfg, int64_t n_frames, int device) {
-    const int64_t need = (n_frames + PK_FRAMES - 1) / PK_FRAMES;
-    const void *k = cfg.est != OFDM_EST_LS ? reinterpret_cast<const void *>(&rx_pack_kernel<0, OFDM_CONV_C, OFDM_CHAN_AWGN, false>)
-                  : cfg.channel == OFDM_CHAN_RAYLEIGH4
-                      ? reinterpret_cast<const void *>(&rx_pack_kernel<2, OFDM_CONV_C, OFDM_CHAN_RAYLEIGH4, false>)
-                      : reinterpret_cast<const void *>(&rx_pack_kernel<2, OFDM_CONV_C, OFDM_CHAN_AWGN, false>);
-    int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1) cus = 256;
-    const int64_t cap = (int64_t)per_cu * cus;
-    const int64_t g = need < cap ? need : cap;
-    return (int)(g < 1 ? 1 : g);
+    if (cfg.est != OFDM_EST_LS) return rx_pack_ideal_grid(n_frames, device);
+    return cfg.channel == OFDM_CHAN_RAYLEIGH4 ? pack_grid<fade_kernel>(n_frames, device)
+                                              : pack_grid<ls_kernel>(n_frames, device);
 }
+#endif
 
 }  // namespace ofdm

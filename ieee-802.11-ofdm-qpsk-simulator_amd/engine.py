@@ -125,6 +125,19 @@ class Engine:
                                                 snr.ctypes.data_as(C.c_void_p), len(snr), _ptr(counters)), "rx_frames")
         return counters
 
+    def txrx_frames(self, cfg: Cfg, first_frame: int, n_frames: int, snr_db, tx=None, bits=None, counters=None):
+        """ofdm_txrx_frames: the Tx batch (written to tx / bits) and its receiver pass in one call (one launch
+        for the packed real-noise receivers)."""
+        snr = np.ascontiguousarray(snr_db, np.float64)
+        if tx is None or bits is None:
+            tx, bits = self.tx_buffers(n_frames)
+        if counters is None:
+            counters = self.new_counters(len(snr))
+        check(self.lib, self.lib.ofdm_txrx_frames(self.ctx, C.byref(cfg), first_frame, n_frames, _ptr(tx), _ptr(bits),
+                                                  snr.ctypes.data_as(C.c_void_p), len(snr), _ptr(counters)),
+              "txrx_frames")
+        return tx, bits, counters
+
     def rx_frames_dump(self, cfg: Cfg, tx, bits, first_frame: int, n_frames: int, snr_db):
         torch = _torch()
         snr = np.ascontiguousarray(snr_db, np.float64)

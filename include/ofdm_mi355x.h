@@ -133,13 +133,19 @@ int ofdm_rx_frames(ofdm_ctx *ctx, const ofdm_cfg *cfg, const void *d_tx, const v
                    uint64_t first_frame, int64_t n_frames, const double *snr_db, int n_snr,
                    void *d_counters);
 /* Pipelining: the NEXT ofdm_rx_frames / ofdm_rx_frames_dump call on ctx also builds this Tx batch
- * (exactly what ofdm_tx_frames with the same arguments writes).  The packed real-noise LS receivers build
- * it in their group prologues on the block's otherwise idle waves; any other call launches ofdm_tx_frames on
+ * (exactly what ofdm_tx_frames with the same arguments writes).  The packed real-noise receivers build it
+ * in their group prologues on the block's otherwise idle waves; any other call launches ofdm_tx_frames on
  * the context's stream first.  The batch must not be the one that call reads.  One batch is pending at a
  * time (a second call replaces it).  An rx call that fails its argument checks leaves the batch pending;
  * ofdm_symbol_sweep builds a pending batch (Tx kernel, context stream) before its own work. */
 int ofdm_set_next_tx(ofdm_ctx *ctx, const ofdm_cfg *cfg, uint64_t first_frame, int64_t n_frames,
                      void *d_tx, void *d_bits);
+/* Tx + Rx of one batch in one call: writes exactly what ofdm_tx_frames(cfg, first_frame, n_frames, d_tx,
+ * d_bits) writes and adds exactly what ofdm_rx_frames on that batch adds.  The packed real-noise receivers
+ * build each group's symbols in their group prologue and read them back (one launch); the others launch
+ * the Tx kernel first.  A pending ofdm_set_next_tx batch is built as by ofdm_rx_frames. */
+int ofdm_txrx_frames(ofdm_ctx *ctx, const ofdm_cfg *cfg, uint64_t first_frame, int64_t n_frames, void *d_tx,
+                     void *d_bits, const double *snr_db, int n_snr, void *d_counters);
 /* Per-symbol dump for parity tests: equalised data subcarriers d_eq [n_snr][n_frames][2][48] float2
  * and demodulated bits d_dbits [n_snr][n_frames][2][3] uint32 (MSB-first). */
 int ofdm_rx_frames_dump(ofdm_ctx *ctx, const ofdm_cfg *cfg, const void *d_tx, const void *d_bits,
@@ -147,10 +153,11 @@ int ofdm_rx_frames_dump(ofdm_ctx *ctx, const ofdm_cfg *cfg, const void *d_tx, co
                         void *d_counters, void *d_eq, void *d_dbits);
 /* Whole sweep ("main()" SNR loop, OFDM.c:1187-1222): Tx + Rx in device-resident chunks of at most
  * chunk_frames frames (0: 2^22, and at least 4 chunks when n_frames >= 2^20); writes host counters
- * [n_snr][OFDM_NCOUNTERS].  With more than one chunk the Tx of chunk k+1 overlaps the receiver of chunk
- * k (double-buffered Tx batches): real-noise LS sweeps build it inside that receiver (ofdm_set_next_tx),
- * the others run it on a second stream owned by the context, ordered by events against the context's
- * stream.  The counters do not depend on the chunking. */
+ * [n_snr][OFDM_NCOUNTERS].  Real-noise sweeps on the packed receivers build every batch inside the
+ * receivers: chunk 0's its own (ofdm_txrx_frames), chunk k's the batch of chunk k+1 (ofdm_set_next_tx,
+ * double-buffered).  The others run the Tx of chunk k+1 on a second stream owned by the context, ordered by
+ * events against the context's stream, under the receiver of chunk k.  The counters do not depend on the
+ * chunking. */
 int ofdm_symbol_sweep(ofdm_ctx *ctx, const ofdm_cfg *cfg, const double *snr_db, int n_snr,
                       uint64_t first_frame, int64_t n_frames, int64_t chunk_frames,
                       int64_t *counters);

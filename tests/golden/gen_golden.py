@@ -3,7 +3,7 @@
 unmodified /root/reference/src/OFDM.c) and from the reference's own data files.
 
 Run in the build container (the GPU box has no /root/reference):
-    python tests/golden/gen_golden.py [--mc-trials 10000]
+    python tests/golden/gen_golden.py [--only mc] [--mc-trials 48000 --mc-deep-trials 1000000]
 
 Outputs (all plain data, loadable with numpy allow_pickle=False / json):
   fft_vectors.npz      200 random 64-pt inputs and the reference's fft()/ifft() outputs (OFDM.c:314-339)
@@ -135,42 +135,78 @@ def gen_genie(R: RefLib, frames: int = 20000, snrs=(0.0, 2.0, 4.0, 6.0)):
     (HERE / "ref_genie_ls_curve.json").write_text(json.dumps(meta, indent=1))
 
 
+MC_SNRS = list(range(0, 17)) + [18, 20, 22, 24, 26, 28, 30]
+MC_DEEP_SNRS = (11, 12, 13, 14, 15)     # the BER waterfall, where the curve is set by rare sync failures
+MC_DEEP_SCALE = {13: 4, 14: 4}          # x --mc-deep-trials where the 1e-3.5 / 1e-4 crossings are pinned
+MC_DEEP_JOB = 25_000                    # trials per deep job (seeded by job index: independent of --procs)
+
+
 def _mc_worker(args):
     snr, n, seed = args
     R = RefLib()
-    t, acc = R.time_trials(snr, n, seed)
+    t, acc = R.mc_trials(snr, n, seed)
     return snr, n, t, acc.tolist()
 
 
-def gen_mc(trials: int, procs: int):
-    snrs = list(range(0, 17)) + [18, 20, 22, 24, 26, 28, 30]
+def mc_jobs(trials: int, procs: int, deep_trials: int, deep_snrs=MC_DEEP_SNRS):
+    """(snr, trials, seed) jobs.  Shallow points: `procs` jobs of trials // procs each, seeded
+    1000003 (p + 1) + snr (the round-2 fixture's seeds: 48000 = 8 x 6000 reproduces its rows).  Deep
+    points: deep_trials (x MC_DEEP_SCALE) in jobs of MC_DEEP_JOB, seeded 2000003 (j + 1) + snr."""
     jobs = []
-    per = max(1, trials // procs)
-    for s in snrs:
-        for p in range(procs):
-            jobs.append((float(s), per, 1000003 * (p + 1) + int(s)))
+    for s in MC_SNRS:
+        if deep_trials and s in deep_snrs:
+            n_jobs = MC_DEEP_SCALE.get(s, 1) * deep_trials // MC_DEEP_JOB
+            jobs += [(float(s), MC_DEEP_JOB, 2000003 * (j + 1) + s) for j in range(n_jobs)]
+        else:
+            per = max(1, trials // procs)
+            jobs += [(float(s), per, 1000003 * (p + 1) + s) for p in range(procs)]
+    return jobs
+
+
+def gen_mc(trials: int, procs: int, deep_trials: int):
+    jobs = mc_jobs(trials, procs, deep_trials)
+    jobs.sort(key=lambda j: -j[1])                      # long jobs first
     with mp.Pool(procs) as pool:
-        res = pool.map(_mc_worker, jobs)
+        res = list(pool.imap_unordered(_mc_worker, jobs, chunksize=1))
     curve = {}
+    keys = ("sum_evm_db", "sum_evm_agc_db", "sum_ber", "sum_ber2", "trials_ber_pos", "trials_ber_ge_quarter",
+            "sum_evm_db2", "trials_evm_agc_finite")
     for snr, n, t, acc in res:
-        c = curve.setdefault(snr, {"trials": 0, "sum_evm_db": 0.0, "sum_evm_agc_db": 0.0, "sum_ber": 0.0, "sec": 0.0})
-        c["trials"] += n; c["sum_evm_db"] += acc[0]; c["sum_evm_agc_db"] += acc[1]; c["sum_ber"] += acc[2]
+        c = curve.setdefault(snr, {"trials": 0, "sec": 0.0, **{k: 0.0 for k in keys}})
+        c["trials"] += n
         c["sec"] += t
+        for k, v in zip(keys, acc):
+            c[k] += v
     rows = []
     for snr in sorted(curve):
         c = curve[snr]
-        rows.append({"snr_db": snr, "trials": c["trials"], "ber": c["sum_ber"] / c["trials"],
-                     "mean_evm_db": c["sum_evm_db"] / c["trials"],
-                     "mean_evm_agc_db": c["sum_evm_agc_db"] / c["trials"],
-                     "sec_per_trial": c["sec"] / c["trials"]})
-    meta = {"generator": "tests/golden/gen_golden.py", "source": "reference OFDM.c (gcc -O2) TOA+Receiver loop",
-            "rand": "64-bit LCG hook (oracle/ref_harness.c)", "rows": rows}
+        n = c["trials"]
+        var_ber = max(c["sum_ber2"] / n - (c["sum_ber"] / n) ** 2, 0.0)
+        rows.append({"snr_db": snr, "trials": n, "ber": c["sum_ber"] / n,
+                     "ber_trial_var": var_ber,                       # per-trial BER variance (frame-clustered)
+                     "trials_ber_pos": int(c["trials_ber_pos"]),      # trials with any bit error
+                     "trials_ber_ge_quarter": int(c["trials_ber_ge_quarter"]),   # failed frames (sync loss)
+                     "mean_evm_db": c["sum_evm_db"] / n,
+                     "evm_db_trial_var": max(c["sum_evm_db2"] / n - (c["sum_evm_db"] / n) ** 2, 0.0),
+                     "mean_evm_agc_db": c["sum_evm_agc_db"] / n,
+                     "trials_evm_agc_finite": int(c["trials_evm_agc_finite"]),
+                     "sec_per_trial": c["sec"] / n})
+    meta = {"generator": f"tests/golden/gen_golden.py --only mc --mc-trials {trials} --procs {procs} "
+                         f"--mc-deep-trials {deep_trials}",
+            "source": "reference OFDM.c (gcc -O2) TOA+Receiver loop (ref_harness.c ref_mc_trials)",
+            "rand": "64-bit LCG hook (oracle/ref_harness.c)",
+            "seeds": "shallow points: 1000003 (p + 1) + snr per process p; deep points "
+                     f"{list(MC_DEEP_SNRS)} (x {MC_DEEP_SCALE} trials): {MC_DEEP_JOB}-trial jobs seeded "
+                     "2000003 (j + 1) + snr",
+            "rows": rows}
     (HERE / "ref_mc_curve.json").write_text(json.dumps(meta, indent=1))
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mc-trials", type=int, default=8000)
+    # the defaults reproduce the committed ref_mc_curve.json (48000 trials/point, 1e6 at 11, 12, 15 dB, 4e6 at 13, 14)
+    ap.add_argument("--mc-trials", type=int, default=48000)
+    ap.add_argument("--mc-deep-trials", type=int, default=1_000_000)
     ap.add_argument("--procs", type=int, default=8)
     ap.add_argument("--skip-mc", action="store_true")
     ap.add_argument("--only", choices=["genie", "mc"], help="regenerate one fixture only")
@@ -181,11 +217,11 @@ def main():
         gen_genie(R)
         return
     if a.only == "mc":
-        gen_mc(a.mc_trials, a.procs)
+        gen_mc(a.mc_trials, a.procs, a.mc_deep_trials)
         return
     gen_fft(R); gen_tx(R); gen_rx(R); gen_kat(); gen_genie(R)
     if not a.skip_mc:
-        gen_mc(a.mc_trials, a.procs)
+        gen_mc(a.mc_trials, a.procs, a.mc_deep_trials)
     print("golden fixtures written to", HERE)
 
 

@@ -220,3 +220,59 @@ def test_pending_next_tx_survives_a_failed_rx_and_is_built_by_symbol_sweep(engin
     engine.set_next_tx(cfg, 4096, 300, tx, bits)
     engine.symbol_sweep(cfg, [5.0], 1000)                # flushes the pending batch first
     assert same(tx, bits)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kw", [dict(conv="c", payload="random"), dict(conv="matlab", payload="message"),
+                                dict(conv="c", payload="tester", channel="rayleigh4"),
+                                dict(conv="c", payload="random", est="ideal"),
+                                dict(conv="matlab", payload="random", est="ideal"),
+                                dict(conv="c", payload="random", noise="complex")])    # not packed: Tx launch
+def test_txrx_equals_tx_then_rx(engine, pkg, kw):
+    """ofdm_txrx_frames: the packed receivers build each group's own symbols in the group prologue and read
+    them back in the same launch.  The batch is byte-identical to the Tx kernel's and the counters equal
+    ofdm_rx_frames on that batch, for ragged sizes (tail groups split over blocks build their group more than
+    once), more SNR points than one launch holds (later launches read the batch the first one built), and
+    with a pending ofdm_set_next_tx batch built in the same launch."""
+    import torch
+    cfg = pkg.make_cfg(**{"est": "ls", "noise": "real", **kw})
+    for first, n, snr in ((5, 1000, [0.0, 10.0]), (3006, 333, list(np.arange(0.0, 40.0, 2.0))), (7, 64, [4.0]),
+                          (11, 40_000, [2.0, 8.0])):
+        tx_ref, bits_ref = engine.tx_frames(cfg, first, n)
+        want = engine.rx_frames(cfg, tx_ref, bits_ref, first, n, snr).cpu().numpy()
+        tx, bits = engine.tx_buffers(n)
+        tx.fill_(-1.0)
+        bits.fill_(-1)
+        nx_ref, nxb_ref = engine.tx_frames(cfg, first + n, 700)
+        nx, nxb = engine.tx_buffers(700)
+        nx.fill_(-1.0)
+        nxb.fill_(-1)
+        engine.set_next_tx(cfg, first + n, 700, nx, nxb)
+        _, _, cnt = engine.txrx_frames(cfg, first, n, snr, tx, bits)
+        torch.cuda.synchronize()
+        assert np.array_equal(cnt.cpu().numpy(), want), (kw, first, n)
+        for (a, b), nf in (((tx_ref, tx), n), ((nx_ref, nx), 700)):
+            n_sym = (2 * nf + 63) // 64 * 64
+            ga = a.view(torch.uint8).cpu().numpy().reshape(80, -1)[:, :8 * n_sym]
+            gb = b.view(torch.uint8).cpu().numpy().reshape(80, -1)[:, :8 * n_sym]
+            assert np.array_equal(ga, gb), (kw, first, n, nf)
+        for (a, b), nf in (((bits_ref, bits), n), ((nxb_ref, nxb), 700)):
+            n_sym = (2 * nf + 63) // 64 * 64
+            assert np.array_equal(a.cpu().numpy().reshape(10, -1)[:, :n_sym], b.cpu().numpy().reshape(10, -1)[:, :n_sym])
+
+
+@pytest.mark.gpu
+def test_pipelined_ideal_step_equals_symbol_sweep(engine, pkg):
+    """c2's step (ideal CSI, fused Tx: one txrx launch per chunk 0) against one ofdm_symbol_sweep"""
+    import torch
+    b = _bench()
+    cfg = pkg.make_cfg(est="ideal", noise="real", channel="awgn", conv="c", payload="random")
+    for first, frames in ((1000, b.PIPE_CHUNKS * b.MIN_PIPE_FRAMES + 77), (3, 500_000)):
+        chunks = b.plan_chunks(first, frames)
+        counters = engine.new_counters(len(b.SNR_GRID))
+        step = b.PipelinedSymbolStep(torch, engine, cfg, chunks, counters, 0, fused=True)
+        for _ in range(2):
+            step()
+        torch.cuda.synchronize()
+        want = engine.symbol_sweep(cfg, b.SNR_GRID, frames, first_frame=first)
+        assert np.array_equal(counters.cpu().numpy(), want)

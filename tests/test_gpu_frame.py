@@ -2,7 +2,6 @@
 and the batched frame sweep, against the compiled reference's golden outputs, the MATLAB
 known-answer vector and the oracle."""
 import json
-import math
 
 import numpy as np
 import pytest
@@ -232,25 +231,57 @@ def _snr_at(snr, ber, level):
     return None
 
 
+def _gpu_ber_batches(engine, pkg, snr, batches, per_batch):
+    """per-batch BER (bit errors / bits) and frame-error counts of the GPU frame sweep"""
+    cfg = pkg.make_cfg(payload="message")
+    ber, ferr = [], []
+    for k in range(batches):
+        c = engine.frame_sweep(cfg, snr, per_batch, first_trial=k * per_batch)
+        ber.append(c[:, 3] / c[:, 2])
+        ferr.append(c[:, 4])
+    return np.array(ber), np.sum(ferr, axis=0)
+
+
 @pytest.mark.slow
 def test_reference_ber_curve_within_tenth_db(engine, pkg):
-    """north_star: reproduce the reference BER-vs-SNR curve within +-0.1 dB.  Reference curve =
-    the compiled OFDM.c's own trial loop, 48000 trials/point (ref_mc_curve.json); GPU: 200k trials."""
-    rows = [r for r in json.loads((GOLDEN / "ref_mc_curve.json").read_text())["rows"] if r["snr_db"] <= 14]
+    """north_star: reproduce the reference BER-vs-SNR curve within +-0.1 dB, down the waterfall.
+
+    Reference: the compiled OFDM.c's own trial loop (ref_mc_curve.json; 48000 trials/point, 1e6 at
+    11..15 dB where the curve is set by rare silent sync failures, OFDM.c:752-761, BER OFDM.c:1152-1161,
+    loop OFDM.c:1195-1222).  GPU: 4e6 trials/point in 20 batches.  The SNR where log10 BER crosses each
+    level (log-linear interpolation between the 1-dB points) must agree within 0.1 dB at every level from
+    10^-1 down to the deepest one whose two bracketing reference points each hold >= 100 failed frames
+    (10^-4 with the 1e6-trial rows).  Point-wise, the two means agree within 5 frame-clustered standard
+    errors: the reference's from its per-trial BER variance (a failed sync costs ~half the bits at once)
+    plus a pseudo-count of one failed frame, the GPU's from the spread of its 20 batches."""
+    rows = [r for r in json.loads((GOLDEN / "ref_mc_curve.json").read_text())["rows"] if r["snr_db"] <= 15]
     snr = np.array([r["snr_db"] for r in rows])
     ref = np.array([r["ber"] for r in rows])
-    n_ref = np.array([r["trials"] for r in rows])
-    c = engine.frame_sweep(pkg.make_cfg(payload="message"), snr, 200_000)
-    ber = c[:, 3] / c[:, 2]
-    for level in (-1.0, -1.5, -2.0, -2.5):
+    n_ref = np.array([r["trials"] for r in rows], float)
+    fails = np.array([r["trials_ber_pos"] for r in rows])
+    K, B = 20, 200_000
+    bb, ferr = _gpu_ber_batches(engine, pkg, snr, K, B)
+    ber = bb.mean(axis=0)
+    se_gpu = bb.std(axis=0, ddof=1) / np.sqrt(K)
+    se_ref = np.sqrt((np.array([r["ber_trial_var"] for r in rows]) * n_ref + 0.25) / n_ref ** 2)
+    checked = []
+    for level in np.arange(-1.0, -6.01, -0.5):
         s_ref, s_gpu = _snr_at(snr, ref, level), _snr_at(snr, ber, level)
-        assert s_ref is not None and s_gpu is not None
-        print(f"BER 1e{level}: reference {s_ref:.3f} dB, GPU {s_gpu:.3f} dB, offset {s_gpu - s_ref:+.3f} dB")
+        if s_ref is None:
+            break
+        i = int(np.searchsorted(snr, s_ref))            # bracketing reference points i - 1, i
+        if min(fails[i - 1], fails[i]) < 100:
+            break
+        assert s_gpu is not None, level
+        print(f"BER 1e{level:+.1f}: reference {s_ref:.3f} dB, GPU {s_gpu:.3f} dB, offset {s_gpu - s_ref:+.3f} dB "
+              f"(reference failed frames {fails[i - 1]} / {fails[i]})")
         assert abs(s_ref - s_gpu) < 0.1, (level, s_ref, s_gpu)
-    # and point-wise within the sampling error (frame-clustered: a failed sync costs ~half the bits)
-    for s, b, r, n in zip(snr, ber, ref, n_ref):
-        sd = math.sqrt(max(r, 1e-4) * 0.5 / n + max(b, 1e-4) * 0.5 / 200_000)
-        assert abs(b - r) < 6 * sd + 2e-4, (s, b, r)
+        checked.append(level)
+    assert min(checked) <= -3.5, checked                # the waterfall, not just its shoulder
+    for s, b, r, eg, er, fe in zip(snr, ber, ref, se_gpu, se_ref, ferr):
+        z = (b - r) / np.hypot(eg, er)
+        print(f"{s:5.1f} dB  BER GPU {b:.4e}  reference {r:.4e}  z {z:+.2f}  GPU frame errors {fe}")
+        assert abs(z) < 5, (s, b, r, eg, er)
 
 
 def test_reference_main_evm_files_vs_reference_curve(pkg, tmp_path):
