@@ -274,11 +274,12 @@ def cpu_baseline(workload: str, seconds: float = 12.0, share: dict | None = None
             "single_core": single}
 
 
-def plan_chunks(first: int, frames: int) -> list[tuple[int, int]]:
+def plan_chunks(first: int, frames: int, n_chunks: int = 0) -> list[tuple[int, int]]:
     """Equal chunks (no small tail launch) of at most MAX_CHUNK_FRAMES frames, and at least PIPE_CHUNKS of
-    them (each >= MIN_PIPE_FRAMES) so that the HBM-bound Tx pass of chunk k+1 can run on a second stream
-    under the VALU-bound receiver of chunk k."""
-    n_chunks = max(PIPE_CHUNKS if frames >= PIPE_CHUNKS * MIN_PIPE_FRAMES else 1, -(-frames // MAX_CHUNK_FRAMES))
+    them (each >= MIN_PIPE_FRAMES) so that the Tx of chunk k+1 can be built under the receiver of chunk k
+    (n_chunks > 0: that many, at least as many as MAX_CHUNK_FRAMES needs)."""
+    auto = PIPE_CHUNKS if frames >= PIPE_CHUNKS * MIN_PIPE_FRAMES else 1
+    n_chunks = max(n_chunks or auto, -(-frames // MAX_CHUNK_FRAMES))
     cut = [first + frames * k // n_chunks for k in range(n_chunks + 1)]
     return [(cut[k], cut[k + 1] - cut[k]) for k in range(n_chunks) if cut[k + 1] > cut[k]]
 
@@ -350,6 +351,7 @@ def main():
                     help="override data symbols per SNR point (per GPU for weak workloads, total for strong)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--chunks", type=int, default=0, help="Tx/receiver chunks per step (0: plan_chunks)")
     ap.add_argument("--pipeline", choices=("auto", "fused", "streams"), default="auto",
                     help="next chunk's Tx: fused into the LS receiver (auto for real-noise LS) or a second stream")
     args = ap.parse_args()
@@ -385,7 +387,7 @@ def main():
     eng = pkg.Engine(dev)
     frame_mode = args.workload == "frame"
     counters = eng.new_counters(len(SNR_GRID))
-    chunks = plan_chunks(first, frames)
+    chunks = plan_chunks(first, frames, args.chunks)
     # real-noise sweeps on the packed receivers (c2, c3, c4, c5): every Tx batch built inside the receivers
     packed = kw.get("noise") == "real" and (kw.get("channel") == "awgn" or kw.get("est") == "ls")
     fused = packed if args.pipeline == "auto" else args.pipeline == "fused"

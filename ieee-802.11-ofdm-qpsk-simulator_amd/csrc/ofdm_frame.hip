@@ -476,7 +476,7 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
             const uint32_t pb = (uint32_t)(a.wave_len / (4 * FR_REPS)), nb_wave = (uint32_t)(a.wave_len / 4);
             uint32_t bm = (uint32_t)(b0 + lane) % pb;
 #ifndef FRAME_CAP_U
-#define FRAME_CAP_U 3
+#define FRAME_CAP_U 6   // Philox blocks per lane per pass: 12 of a reference capture in 2 passes (A/B: +0.8 % over 3)
 #endif
             for (int bb = b0 + lane; bb <= b1; bb += FRAME_CAP_U * 64) {
                 float4 v[FRAME_CAP_U];
@@ -1018,7 +1018,13 @@ static unsigned occupancy_grid(const void *kernel, int threads, size_t lds, int 
     return (unsigned)std::max<int64_t>(1, std::min<int64_t>(blocks, (int64_t)per_cu * cus * waves));
 }
 
-constexpr int64_t FRAME_CHUNK_ITEMS = int64_t(1) << 18;   // items per sync -> symbol hand-off (<= 1 GB)
+// items per sync -> symbol hand-off: 2^22 items x 2 KB (reference message) = 8 GB of HBM, one launch pair per
+// 4M items (A/B, frame mode: 2^18 3.13e8, 2^20 3.33e8, 2^22 3.40e8 symbol-SNR/s -- each pair ends in a tail
+// and K4b' waits for K4b)
+#ifndef FRAME_CHUNK_LOG2
+#define FRAME_CHUNK_LOG2 22
+#endif
+constexpr int64_t FRAME_CHUNK_ITEMS = int64_t(1) << FRAME_CHUNK_LOG2;
 
 // K4b then K4b' over a.n_items items starting at a.item0, through the context's hand-off buffer
 static int run_frame_chunk(Ctx *c, FrameArgs &a) {
