@@ -1,6 +1,7 @@
 """bench.py's step plan (CPU) and its pipelined symbol step against one ofdm_symbol_sweep (GPU): the
 benchmark's own code path must produce the counters a plain sweep produces."""
 import importlib.util
+import sys
 
 import numpy as np
 import pytest
@@ -9,10 +10,13 @@ from conftest import ROOT
 
 
 def _bench():
-    spec = importlib.util.spec_from_file_location("bench", ROOT / "bench.py")
-    mod = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(mod)
-    return mod
+    """bench.py as the module `bench` (one instance: its cpu_baseline workers are pickled by reference)"""
+    if "bench" not in sys.modules:
+        spec = importlib.util.spec_from_file_location("bench", ROOT / "bench.py")
+        mod = importlib.util.module_from_spec(spec)
+        sys.modules["bench"] = mod
+        spec.loader.exec_module(mod)
+    return sys.modules["bench"]
 
 
 @pytest.mark.parametrize("first,frames", [(0, 0), (0, 7), (5, 1_000_000), (0, 1 << 20), (123, 5_000_000),
