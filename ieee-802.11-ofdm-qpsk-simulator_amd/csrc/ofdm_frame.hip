@@ -370,18 +370,20 @@ __device__ __forceinline__ int im_mod(const A &a, int x) {
     return x - (int)(q * (uint32_t)a.im_period);
 }
 
-// 21 contiguous LDS floats p[s .. s + 20] into x[20 - t] = p[s + t] order reversed (x[t] = sample n - t for
-// s = n - 20), as 10 ds_read_b64 + 1 ds_read_b32; ODD = s & 1 (uniform per item: the pairs are 8-byte aligned)
-template <int ODD>
-__device__ __forceinline__ void lds_read21(const float *p, int s, float (&x)[21]) {
+// N (odd) contiguous LDS floats x[k] = p[s + k] as (N - 1) / 2 ds_read_b64 + 1 ds_read_b32; ODD = s & 1 (uniform
+// per item), so the pairs are 8-byte aligned
+template <int ODD, int N>
+__device__ __forceinline__ void lds_readn(const float *p, int s, float (&x)[N]) {
+    static_assert(N & 1, "odd window");
+    if constexpr (ODD) x[0] = p[s];
     const float2 *q = reinterpret_cast<const float2 *>(p + s + ODD);
 #pragma unroll
-    for (int m = 0; m < 10; ++m) {
-        const float2 w = q[m];                       // floats s + ODD + 2m, s + ODD + 2m + 1
-        x[20 - ODD - 2 * m] = w.x;
-        x[19 - ODD - 2 * m] = w.y;
+    for (int m = 0; m < (N - 1) / 2; ++m) {
+        const float2 w = q[m];                           // floats s + ODD + 2m, s + ODD + 2m + 1
+        x[ODD + 2 * m] = w.x;
+        x[ODD + 2 * m + 1] = w.y;
     }
-    x[ODD ? 20 : 0] = p[ODD ? s : s + 20];
+    if constexpr (!ODD) x[N - 1] = p[s + N - 1];
 }
 
 #ifndef FRAME_SYNC_MINW
@@ -681,19 +683,18 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
 #pragma unroll
             for (int j = 0; j < 11; ++j) asm volatile("v_mov_b32 %0, %1" : "=v"(tv[j]) : "s"(tp[j]));
         }
-        const int nmf = dbg ? nfr : 160 + 64 * a.n_data;
         // parities of the first float of a filter window in the region and in the table: uniform per item
         // (n = p + 2 ii; the period is even)
         const int par_r = (off + p) & 1, par_i = (im0 + p) & 1;
-        for (int j = lx; j < nmf; j += 64) {
-            const int ii = dbg ? j : needed_k(j);
+        // one output at frame instant ii (the per-instant path: windows that leave the capture, the dump)
+        auto mf_one = [&](int ii) {
             const int n = p + 2 * ii;
             float2 v = make_float2(0.f, 0.f);
             if (n >= 20 && n < L) {                              // all 21 taps inside the capture
-                float xr[21], xi[21];                            // x[t] = sample n - t
+                float xr[21], xi[21];                            // x[20 - t] = sample n - t
                 const int si = im_mod(a, im0 + n - 20);
-                if (par_r) lds_read21<1>(rbase, off + n - 20, xr); else lds_read21<0>(rbase, off + n - 20, xr);
-                if (par_i) lds_read21<1>(imt, si, xi); else lds_read21<0>(imt, si, xi);
+                if (par_r) lds_readn<1>(rbase, off + n - 20, xr); else lds_readn<0>(rbase, off + n - 20, xr);
+                if (par_i) lds_readn<1>(imt, si, xi); else lds_readn<0>(imt, si, xi);
                 v = make_float2(xr[10] * tv[10], xi[10] * tv[10]);
 #pragma unroll
                 for (int tt = 0; tt < 10; ++tt) {
@@ -715,6 +716,51 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
                 }
             }
             fr[ii] = v;                                          // outside every lane's reads
+        };
+        if (dbg) {
+            for (int j = lx; j < nfr; j += 64) mf_one(j);
+        } else {
+            // runs of MF_RUN consecutive instants inside one needed range ([80, 112) the coarse-CFO lag window,
+            // [192, 320) both LTFs, [336 + 80 d, +64) the data windows): a run's outputs share their samples, so
+            // a lane loads 2 MF_RUN + 19 samples per run instead of 21 per output (58 instead of 210 LDS
+            // floats for 5 outputs).  One run per lane and pass (59 runs for the reference message).
+            constexpr int MF_RUN = 5, MF_W = 2 * MF_RUN + 19;
+            constexpr int c0 = (32 + MF_RUN - 1) / MF_RUN, c1 = c0 + (128 + MF_RUN - 1) / MF_RUN;
+            constexpr int cd = (64 + MF_RUN - 1) / MF_RUN;
+            const int n_runs = c1 + cd * a.n_data;
+            for (int u = lx; u < n_runs; u += 64) {
+                int s0, e;
+                if (u < c0) {
+                    s0 = 80 + MF_RUN * u; e = 112;
+                } else if (u < c1) {
+                    s0 = 192 + MF_RUN * (u - c0); e = 320;
+                } else {
+                    const int d = (u - c1) / cd, k = u - c1 - d * cd;
+                    s0 = 336 + 80 * d + MF_RUN * k; e = 400 + 80 * d;
+                }
+                e = min(e, s0 + MF_RUN);
+                const int n_lo = p + 2 * s0 - 20;                // first sample read
+                if (n_lo >= 0 && p + 2 * (e - 1) < L) {
+                    float xr[MF_W], xi[MF_W];                    // x[k] = sample n_lo + k
+                    const int si = im_mod(a, im0 + n_lo);
+                    if (par_r) lds_readn<1>(rbase, off + n_lo, xr); else lds_readn<0>(rbase, off + n_lo, xr);
+                    if (par_i) lds_readn<1>(imt, si, xi); else lds_readn<0>(imt, si, xi);
+#pragma unroll
+                    for (int o = 0; o < MF_RUN; ++o) {           // output at sample n_lo + 2 o + 20
+                        if (s0 + o < e) {
+                            float2 v = make_float2(xr[2 * o + 10] * tv[10], xi[2 * o + 10] * tv[10]);
+#pragma unroll
+                            for (int tt = 0; tt < 10; ++tt) {
+                                v.x = fmaf(xr[2 * o + 20 - tt] + xr[2 * o + tt], tv[tt], v.x);
+                                v.y = fmaf(xi[2 * o + 20 - tt] + xi[2 * o + tt], tv[tt], v.y);
+                            }
+                            fr[s0 + o] = v;
+                        }
+                    }
+                } else {
+                    for (int ii = s0; ii < e; ++ii) mf_one(ii);
+                }
+            }
         }
         const bool oob = __ballot(oob_l) != 0ull;
         wave_lds_sync();

@@ -247,19 +247,19 @@ def test_reference_ber_curve_within_tenth_db(engine, pkg):
     """north_star: reproduce the reference BER-vs-SNR curve within +-0.1 dB, down the waterfall.
 
     Reference: the compiled OFDM.c's own trial loop (ref_mc_curve.json; 48000 trials/point, 1e6 at
-    11..15 dB where the curve is set by rare silent sync failures, OFDM.c:752-761, BER OFDM.c:1152-1161,
-    loop OFDM.c:1195-1222).  GPU: 4e6 trials/point in 20 batches.  The SNR where log10 BER crosses each
-    level (log-linear interpolation between the 1-dB points) must agree within 0.1 dB at every level from
-    10^-1 down to the deepest one whose two bracketing reference points each hold >= 100 failed frames
-    (10^-4 with the 1e6-trial rows).  Point-wise, the two means agree within 5 frame-clustered standard
-    errors: the reference's from its per-trial BER variance (a failed sync costs ~half the bits at once)
-    plus a pseudo-count of one failed frame, the GPU's from the spread of its 20 batches."""
+    11, 12, 15 dB and 4e6 at 13, 14 dB where the curve is set by rare failed frames, OFDM.c:752-761, BER
+    OFDM.c:1152-1161, loop OFDM.c:1195-1222).  GPU: 1e7 trials/point in 50 batches.  The SNR where log10
+    BER crosses each level (log-linear interpolation between the 1-dB points) must agree within 0.1 dB at
+    every level from 10^-1 down to the deepest one whose two bracketing reference points each hold >= 100
+    trials with errors (10^-4).  Point-wise, the two means agree within 5 frame-clustered standard errors: the reference's from
+    its per-trial BER variance (a failed sync costs ~half the bits at once) plus a pseudo-count of one
+    failed frame, the GPU's from the spread of its 50 batches."""
     rows = [r for r in json.loads((GOLDEN / "ref_mc_curve.json").read_text())["rows"] if r["snr_db"] <= 15]
     snr = np.array([r["snr_db"] for r in rows])
     ref = np.array([r["ber"] for r in rows])
     n_ref = np.array([r["trials"] for r in rows], float)
     fails = np.array([r["trials_ber_pos"] for r in rows])
-    K, B = 20, 200_000
+    K, B = 50, 200_000
     bb, ferr = _gpu_ber_batches(engine, pkg, snr, K, B)
     ber = bb.mean(axis=0)
     se_gpu = bb.std(axis=0, ddof=1) / np.sqrt(K)
