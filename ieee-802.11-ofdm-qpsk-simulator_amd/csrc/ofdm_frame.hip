@@ -321,12 +321,9 @@ __device__ __forceinline__ int needed_k(int j) {
 constexpr int SYNC_WAVES = FRAME_SYNC_WAVES;
 constexpr int SYNC_THREADS = 64 * SYNC_WAVES;
 constexpr int IMT_EXT = 128;         // table slack past one waveform copy: a lane's longest contiguous read
-#ifndef FRAME_DET_B
-#define FRAME_DET_B 5               // detection positions per batch of LDS reads
-#endif
-constexpr int DET_B = FRAME_DET_B;
+constexpr int DET_B = 16;           // detection positions per batch (= samples per register block)
 // detection positions per lane and round: the largest odd chunk whose ceil(chunk / DET_B) batches fit one
-// 64-bit crossing mask (59 for DET_B = 5); at most 2 rounds (captures up to 64 x 2 x 59 + 47 samples)
+// 64-bit crossing mask (63 for DET_B = 16); at most 2 rounds
 constexpr int det_max_chunk() {
     int c = 63;
     while ((c + DET_B - 1) / DET_B * DET_B > 64) c -= 2;
@@ -544,8 +541,8 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
         }
 
         // ---- Packet_Detection (OFDM.c:659-683): M[n] = |sum r[n+k] r[n+k+16]|^2 / (sum |r[n+k+16]|^2)^2,
-        // k < 32, no conjugate, on the UNFILTERED capture; sliding sums over each lane's chunk with the LDS
-        // reads issued DET_B positions at a time.  M > 0.75 (OFDM.c:687, 695) is decided as the sign of
+        // k < 32, no conjugate, on the UNFILTERED capture; sliding sums over each lane's chunk, DET_B
+        // positions per batch.  M > 0.75 (OFDM.c:687, 695) is decided as the sign of
         // t = 0.75 den - num (fma: exact before its one rounding): t < 0 <=> crossing, which keeps the
         // division's outcomes 0/0 -> false (t = +0) and x/0 -> true (t = -num).  Lane l of round rho owns
         // positions [(64 rho + l) chunk, +chunk); crossing n at bit n - n0 of the round's mask. ----
@@ -559,39 +556,55 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
                 const float *ti_ = imt + im_mod(a, im0 + n0);   // Im of sample n0 + k at ti_[k] (k < IMT_EXT)
                 const float *tr_ = r + n0;
                 float sx = 0.f, sy = 0.f, pw = 0.f;
-#pragma unroll 8
-                for (int k = 0; k < 32; ++k) {
-                    const float ux = tr_[k], uy = ti_[k], vx = tr_[k + 16], vy = ti_[k + 16];
-                    sx = fmaf(ux, vx, sx); sx = fmaf(-uy, vy, sx);
-                    sy = fmaf(ux, vy, sy); sy = fmaf(uy, vx, sy);
-                    pw = fmaf(vx, vx, pw); pw = fmaf(vy, vy, pw);
-                }
-                // t's sign bits shifted in with v_alignbit, one per position (first position highest); every
-                // active lane runs the same ceil(chunk / DET_B) batches, positions past n1 are masked below
                 uint32_t mlo = 0u, mhi = 0u;
                 const int nbat = (chunk + DET_B - 1) / DET_B;
-                for (int b = 0; b < nbat; ++b) {
-                    const int nb = DET_B * b;
-                    float o0x[DET_B], o0y[DET_B], o1x[DET_B], o1y[DET_B], i0x[DET_B], i0y[DET_B], i1x[DET_B], i1y[DET_B];
+                // Samples in register blocks of DET_B: position n's window terms read samples n (leaving), n + 16,
+                // n + 32 and n + 48 (entering), i.e. blocks b, b + 1, b + 2, b + 3 of batch b, so every sample is
+                // loaded from LDS once (ds_read2_b32) instead of four times (A/B: +2.3 % frame mode, 167 VGPRs).
+                static_assert(DET_B == 16, "blocks of 16 samples: the 16-sample lag is one block");
+                constexpr int NB = 64 / DET_B;                    // batches per round at most
+                float xr[NB + 3][DET_B], xi[NB + 3][DET_B];
+                auto load_blk = [&](auto jc) {
+                    constexpr int j = decltype(jc)::value;
 #pragma unroll
-                    for (int k = 0; k < DET_B; ++k) {   // reads past the capture land in the region's slack
-                        o0x[k] = tr_[nb + k]; o1x[k] = tr_[nb + k + 16]; i0x[k] = tr_[nb + k + 32]; i1x[k] = tr_[nb + k + 48];
-                        o0y[k] = ti_[nb + k]; o1y[k] = ti_[nb + k + 16]; i0y[k] = ti_[nb + k + 32]; i1y[k] = ti_[nb + k + 48];
-                    }
+                    for (int k = 0; k < DET_B; ++k) { xr[j][k] = tr_[DET_B * j + k]; xi[j][k] = ti_[DET_B * j + k]; }
+                };
+                load_blk(std::integral_constant<int, 0>{});
+                load_blk(std::integral_constant<int, 1>{});
+                load_blk(std::integral_constant<int, 2>{});
+                static_for<0, 2>([&](auto hc) {                    // the first window: k = 16 h + kk
+                    constexpr int h = decltype(hc)::value;
 #pragma unroll
-                    for (int k = 0; k < DET_B; ++k) {
-                        const float num = fmaf(sx, sx, sy * sy), h = 0.75f * pw;
-                        const float tt = fmaf(h, pw, -num);
-                        mhi = __builtin_amdgcn_alignbit(mhi, mlo, 31);
-                        mlo = __builtin_amdgcn_alignbit(mlo, __float_as_uint(tt), 31);
-                        sx = fmaf(i0x[k], i1x[k], sx); sx = fmaf(-i0y[k], i1y[k], sx);
-                        sx = fmaf(-o0x[k], o1x[k], sx); sx = fmaf(o0y[k], o1y[k], sx);
-                        sy = fmaf(i0x[k], i1y[k], sy); sy = fmaf(i0y[k], i1x[k], sy);
-                        sy = fmaf(-o0x[k], o1y[k], sy); sy = fmaf(-o0y[k], o1x[k], sy);
-                        pw = fmaf(i1x[k], i1x[k], pw); pw = fmaf(i1y[k], i1y[k], pw);
-                        pw = fmaf(-o1x[k], o1x[k], pw); pw = fmaf(-o1y[k], o1y[k], pw);
+                    for (int kk = 0; kk < DET_B; ++kk) {
+                        const float ux = xr[h][kk], uy = xi[h][kk], vx = xr[h + 1][kk], vy = xi[h + 1][kk];
+                        sx = fmaf(ux, vx, sx); sx = fmaf(-uy, vy, sx);
+                        sy = fmaf(ux, vy, sy); sy = fmaf(uy, vx, sy);
+                        pw = fmaf(vx, vx, pw); pw = fmaf(vy, vy, pw);
                     }
-                }
+                });
+                // t's sign bits shifted in with v_alignbit, one per position (first position highest); every
+                // active lane runs the same ceil(chunk / DET_B) batches, positions past n1 are masked below
+                static_for<0, NB>([&](auto bc) {
+                    constexpr int b = decltype(bc)::value;
+                    if (b < nbat) {                                // reads past the capture land in the slack
+                        load_blk(std::integral_constant<int, b + 3>{});
+#pragma unroll
+                        for (int k = 0; k < DET_B; ++k) {
+                            const float o0x = xr[b][k], o0y = xi[b][k], o1x = xr[b + 1][k], o1y = xi[b + 1][k];
+                            const float i0x = xr[b + 2][k], i0y = xi[b + 2][k], i1x = xr[b + 3][k], i1y = xi[b + 3][k];
+                            const float num = fmaf(sx, sx, sy * sy), h = 0.75f * pw;
+                            const float tt = fmaf(h, pw, -num);
+                            mhi = __builtin_amdgcn_alignbit(mhi, mlo, 31);
+                            mlo = __builtin_amdgcn_alignbit(mlo, __float_as_uint(tt), 31);
+                            sx = fmaf(i0x, i1x, sx); sx = fmaf(-i0y, i1y, sx);
+                            sx = fmaf(-o0x, o1x, sx); sx = fmaf(o0y, o1y, sx);
+                            sy = fmaf(i0x, i1y, sy); sy = fmaf(i0y, i1x, sy);
+                            sy = fmaf(-o0x, o1y, sy); sy = fmaf(-o0y, o1x, sy);
+                            pw = fmaf(i1x, i1x, pw); pw = fmaf(i1y, i1y, pw);
+                            pw = fmaf(-o1x, o1x, pw); pw = fmaf(-o1y, o1y, pw);
+                        }
+                    }
+                });
                 // J = nbat * DET_B <= 64 positions: position j sits at bit J - 1 - j of (mhi:mlo); reverse
                 const int J = nbat * DET_B;
                 const unsigned long long rev = ((unsigned long long)__builtin_bitreverse32(mlo) << 32) |
