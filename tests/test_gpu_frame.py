@@ -326,3 +326,25 @@ def test_reference_main_writes_files(pkg, tmp_path):
     evm = pkg.read_float_array_file(tmp_path / "Output_EVM_AGC.txt")
     assert evm[-1] < -35
     assert res.counters.shape == (35, 16)
+
+
+def test_reference_main_evm_finite_files(pkg, tmp_path):
+    """--evm finite: Output_EVM_AGC_DB.txt holds the mean post-slicer EVM_dB over the trials that have one
+    (finite where any trial had a slicer error), the finite counts go to the sidecar; the pre-slicer file is
+    the default's."""
+    from ofdm_amd import sweep
+    snr = np.arange(6.0, 13.0)
+    (tmp_path / "t").mkdir()
+    (tmp_path / "f").mkdir()
+    res = sweep.reference_main(tmp_path / "t", trials=2000, snr_db=snr)
+    sweep.reference_main(tmp_path / "f", trials=2000, snr_db=snr, evm="finite")
+    pre_t = pkg.read_float_array_file(tmp_path / "t" / "Output_EVM_AGC.txt")
+    pre_f = pkg.read_float_array_file(tmp_path / "f" / "Output_EVM_AGC.txt")
+    post_f = pkg.read_float_array_file(tmp_path / "f" / "Output_EVM_AGC_DB.txt")
+    side = json.loads((tmp_path / "f" / "ofdm_sweep.json").read_text())
+    assert np.array_equal(pre_t, pre_f)
+    fin = np.array(side["post_finite_trials"])
+    assert np.all(fin > 0) and np.all(fin < 2000)            # some trials clean, some with slicer errors
+    assert np.all(np.isfinite(post_f))
+    want = res.counters[:, pkg.abi.C_EVMDB_POST_Q] / pkg.abi.EVM_Q_SCALE / fin
+    assert np.allclose(post_f, [float("%.2e" % np.float32(v)) for v in want], rtol=0, atol=0.006)
