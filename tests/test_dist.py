@@ -1,8 +1,10 @@
 """Multi-process path on CPU (gloo, world_size 2): counter-range sharding + ONE all-reduce of the
 int64 counters gives exactly the single-process result.  Per-rank counters come from
 the oracle (test data source); the GPU ranks use the same dist helpers over RCCL."""
+import json
 import os
 import socket
+from pathlib import Path
 
 import numpy as np
 import pytest
@@ -83,3 +85,44 @@ def test_word_stats_reduce_min_max(tmp_path):
     assert list(t[:, 2]) == [300, 300]
     assert list(t[:, 13]) == [-6 << 20, -1 << 20] and list(t[:, 14]) == [10 << 20, 1 << 19]
     assert list(t[:, 15]) == [5, 1]           # max|.| 10 -> ceil(log2 10) + 1 = 5; 1.0 -> ceil(0) + 1 = 1
+
+
+def _late_rank0_worker(rank, world, port, out_path):
+    """bench.py's order under torchrun: rank 0 times the reference BEFORE it forms the process group (here a
+    real, short cpu_baseline on 2 host processes), the other rank goes straight to init_process_group and
+    waits at the rendezvous; then the counters' all-reduce runs as usual."""
+    import sys
+    import time
+    sys.path.insert(0, str(ROOT))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import argparse
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench", ROOT / "bench.py")
+    bench = importlib.util.module_from_spec(spec)
+    sys.modules["bench"] = bench
+    spec.loader.exec_module(bench)
+    cpu = None
+    t0 = time.perf_counter()
+    if bench.wants_cpu_baseline(argparse.Namespace(no_cpu_baseline=False)):
+        share = {"cores": 2, "affinity": 2, "quota": None, "source": "test", "visible": 2}
+        cpu = bench.cpu_baseline("c3", seconds=0.5, share=share)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    waited = time.perf_counter() - t0
+    t = torch.full((2, 16), rank + 1, dtype=torch.int64)
+    dist.all_reduce(t)
+    if rank == 0:
+        np.save(out_path, t.numpy())
+        Path(out_path).with_suffix(".json").write_text(json.dumps({"cpu": cpu}))
+    else:
+        np.save(str(out_path) + f".{rank}.npy", np.array([waited]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_rank0_times_the_reference_before_the_rendezvous(tmp_path, reflib):
+    out = tmp_path / "late.npy"
+    mp.spawn(_late_rank0_worker, args=(2, _free_port(), str(out)), nprocs=2, join=True)
+    assert np.array_equal(np.load(out), np.full((2, 16), 3))
+    cpu = json.loads(out.with_suffix(".json").read_text())["cpu"]
+    assert cpu["kind"] == "reference" and cpu["cores"] == 2 and cpu["value"] > 0
+    assert np.load(str(out) + ".1.npy")[0] > 0.3          # rank 1 waited at the rendezvous for rank 0
