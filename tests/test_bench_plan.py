@@ -236,12 +236,13 @@ def test_txrx_equals_tx_then_rx(engine, pkg, kw):
     """ofdm_txrx_frames: the packed receivers build each group's own symbols in the group prologue and read
     them back in the same launch.  The batch is byte-identical to the Tx kernel's and the counters equal
     ofdm_rx_frames on that batch, for ragged sizes (tail groups split over blocks build their group more than
-    once), more SNR points than one launch holds (later launches read the batch the first one built), and
-    with a pending ofdm_set_next_tx batch built in the same launch."""
+    once), more groups than the grid has blocks (a block builds its next item's group in the prologue of the
+    item before), more SNR points than one launch holds (later launches read the batch the first one built),
+    and with a pending ofdm_set_next_tx batch built in the same launch."""
     import torch
     cfg = pkg.make_cfg(**{"est": "ls", "noise": "real", **kw})
     for first, n, snr in ((5, 1000, [0.0, 10.0]), (3006, 333, list(np.arange(0.0, 40.0, 2.0))), (7, 64, [4.0]),
-                          (11, 40_000, [2.0, 8.0])):
+                          (11, 40_000, [2.0, 8.0]), (13, 120_000, [2.0, 8.0, 14.0])):
         tx_ref, bits_ref = engine.tx_frames(cfg, first, n)
         want = engine.rx_frames(cfg, tx_ref, bits_ref, first, n, snr).cpu().numpy()
         tx, bits = engine.tx_buffers(n)
