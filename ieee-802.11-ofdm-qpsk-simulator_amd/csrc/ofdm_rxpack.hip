@@ -40,6 +40,11 @@ typedef __attribute__((address_space(3))) f2v lf2;
 
 // the LTF noise spectrum E'[k] of the odd-k pairs waits in LDS (per wave) until the odd sub-blocks are
 // consumed: 22 VGPRs less at the register peak (the data FFT's 128 + the even pairs' E')
+#ifndef OFDM_PACK_PF
+// LS AWGN receiver: bin-pair LDS operands loaded this many pairs ahead (A/B, profiles/r03/ab_i: c3 +1.2 % at 2,
+// +0.6 % at 1; the Rayleigh receiver, whose E spectrum is per frame, gains nothing and keeps 0)
+#define OFDM_PACK_PF 2
+#endif
 #ifndef OFDM_PACK_EE_LDS
 #define OFDM_PACK_EE_LDS 24   // 24 = none: no spill without it (222 VGPRs); A/B option
 #endif
@@ -433,6 +438,29 @@ __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_
             asm volatile("v_mov_b32 %0, 0x80000000" : "=v"(sm));
             float evm = 0.f;
             uint32_t em = 0u, be = 0u, ax = 0u, t0 = 0u, t1 = 0u;
+            // LDS operands of a bin pair (both clean spectra and, LS, the E spectrum), loaded PF pairs ahead of
+            // their use so that the read latency is covered by the pairs in between (the fences every
+            // OFDM_PACK_FENCE_PAIRS pairs keep the loads where they are written)
+            constexpr int PF = KIND == 2 && !FADE ? OFDM_PACK_PF : 0;
+            f4v pc0[PF + 1], pc1[PF + 1];
+            float4 pe4[PF + 1];
+            auto load_pair = [&](auto pc) {
+                constexpr int p = decltype(pc)::value;
+                if constexpr (p < PACK_PAIRS) {
+                    constexpr int slot = p % (PF + 1);
+                    pc0[slot] = sp[p * 2 * PK_FRAMES];
+                    pc1[slot] = sp[(p * 2 + 1) * PK_FRAMES];
+                    if constexpr (KIND == 2) {
+                        if constexpr (FADE) {
+                            const f4v v = fp[p * PK_FRAMES];
+                            pe4[slot] = make_float4(v.x, v.y, v.z, v.w);
+                        } else {
+                            pe4[slot] = ce[p];
+                        }
+                    }
+                }
+            };
+            if constexpr (PF > 0) static_for<0, PF>(load_pair);
             auto pair = [&](auto pc) {
                 constexpr int p = decltype(pc)::value;
                 constexpr int k = pair_bin(p), k2 = 64 - k;
@@ -440,9 +468,12 @@ __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_
                     const u2v tt = tw[(p >> 3) * (PK_SYMS / 2)];
                     t0 = tt.x; t1 = tt.y;
                 }
+                if constexpr (PF > 0) load_pair(std::integral_constant<int, p + PF>{});
+                constexpr int slot = p % (PF + 1);
                 const float2 Zk = x[digit_rev4(k)], Zm = x[digit_rev4(k2)];
                 const float2 A = make_float2(Zk.x + Zm.x, Zk.y - Zm.y), B = make_float2(Zk.x - Zm.x, Zk.y + Zm.y);
-                const f4v c0 = sp[p * 2 * PK_FRAMES], c1 = sp[(p * 2 + 1) * PK_FRAMES];
+                if constexpr (PF == 0) load_pair(pc);
+                const f4v c0 = pc0[slot], c1 = pc1[slot];
                 // Y_d = C_d + N_d:  N0[k] = A/2, N0[k'] = conj(A)/2, N1[k] = -j B/2, N1[k'] = conj(N1[k])
                 const float2 y0k = make_float2(fmaf(0.5f, A.x, c0.x), fmaf(0.5f, A.y, c0.y));
                 const float2 y0m = make_float2(fmaf(0.5f, A.x, c0.z), fmaf(-0.5f, A.y, c0.w));
@@ -458,13 +489,7 @@ __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_
                         const f2v v = eew[(p - EE_LDS_FIRST) * 64];
                         ex = v.x; ey = v.y;
                     }
-                    float4 e4;
-                    if constexpr (FADE) {
-                        const f4v v = fp[p * PK_FRAMES];
-                        e4 = make_float4(v.x, v.y, v.z, v.w);
-                    } else {
-                        e4 = ce[p];
-                    }
+                    const float4 e4 = pe4[slot];
                     const float2 Sk = make_float2(fmaf(0.5f, ex, e4.x), fmaf(0.5f, ey, e4.y));
                     const float2 Sm = make_float2(fmaf(0.5f, ex, e4.z), fmaf(-0.5f, ey, e4.w));
                     rk = __builtin_amdgcn_rcpf(fmaf(Sk.x, Sk.x, Sk.y * Sk.y));
