@@ -87,16 +87,25 @@ def kernel_symbols(lib_path) -> dict:
 
 
 def kernel_build_id(lib_path, fragments) -> str | None:
-    """sha256 (first 16 hex digits) over the code and kernel descriptor of every kernel whose mangled name
-    contains one of `fragments`; None when no kernel matches."""
+    """sha256 (first 16 hex digits) over the code and kernel descriptor (its code-entry offset zeroed) of every
+    kernel whose mangled name contains one of `fragments`; None when no kernel matches."""
     syms = kernel_symbols(lib_path)
     names = sorted(n for n in syms if any(re.search(re.escape(f), n) for f in fragments))
     if not names:
         return None
     h = hashlib.sha256()
     for n in names:
-        h.update(n.encode() + b"\0" + syms[n])
+        h.update(n.encode() + b"\0" + _layout_free(n, syms[n]))
     return h.hexdigest()[:16]
+
+
+def _layout_free(name: str, body: bytes) -> bytes:
+    """A kernel descriptor's kernel_code_entry_byte_offset (bytes 16-23: descriptor to code entry) depends on
+    where the linker placed the code, which moves when any other kernel of the library changes size; it is
+    zeroed, so that the id changes with the kernel's own code and descriptor only."""
+    if name.endswith(".kd") and len(body) == 64:
+        return body[:16] + bytes(8) + body[24:]
+    return body
 
 
 def workload_build_id(lib_path, workload: str) -> str | None:

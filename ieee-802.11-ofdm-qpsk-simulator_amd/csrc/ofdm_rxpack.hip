@@ -166,6 +166,19 @@ __device__ __forceinline__ Noise4 pack_noise(const PhiloxHead &hd, uint32_t c2, 
 #endif
 }
 
+#ifdef OFDM_PACK_STAMPS   // diagnostic build: s_memtime per item phase, per wave role, summed over the grid
+#include <cstdio>
+static __device__ unsigned long long g_pack_stamps[4][8];
+#define PK_STAMP(k)                                                                  \
+    do {                                                                             \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                  \
+        st_acc[k] += t_ - st_t;                                                      \
+        st_t = t_;                                                                   \
+    } while (0)
+#else
+#define PK_STAMP(k) do { } while (0)
+#endif
+
 // KIND 2: LS estimate from the LTF pair (E spectrum in LDS `ce`, noise from the packed 32-point FFT);
 // KIND 0: ideal channel knowledge (AWGN), Z = Y (times (-1)^bin for the C ifft convention, D5).
 // CHAN (KIND 2 only): OFDM_CHAN_RAYLEIGH4 applies each frame's 4-tap channel to its clean spectra in the
@@ -176,6 +189,11 @@ __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_
     constexpr bool FADE = CHAN == OFDM_CHAN_RAYLEIGH4;
     static_assert(!FADE || KIND == 2, "the packed Rayleigh receiver is the LS one");
     constexpr bool EEL = KIND == 2 && EE_LDS_N > 0;
+#ifndef OFDM_NO_PACK_WARM_LATE
+    constexpr bool WLATE = KIND == 2 && !FADE;      // where the next item's L2 warm-up is issued (see the SNR loop)
+#else
+    constexpr bool WLATE = false;
+#endif
     __shared__ __attribute__((aligned(16))) float4 spec[PACK_PAIRS][2][PK_FRAMES];   // 48 KB: (C[k], C[64-k])
     __shared__ __attribute__((aligned(16))) float4 ce[PACK_PAIRS];                   // LS: FFT((-1)^n 2T[n])
     __shared__ __attribute__((aligned(16))) float4 fce[FADE ? PACK_PAIRS : 1][FADE ? PK_FRAMES : 1];  // 24 KB: H' FFT(2T)
@@ -185,6 +203,10 @@ __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_
     __shared__ __attribute__((aligned(8))) float2 eel[EEL ? 4 : 1][EEL ? EE_LDS_N : 1][EEL ? 64 : 1];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);      // wave-uniform: the SNR loop runs on SGPRs
+#ifdef OFDM_PACK_STAMPS
+    unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long st_t = __builtin_amdgcn_s_memtime();
+#endif
     for (int i = tid; i < a.n_snr * 5; i += blockDim.x) (&sacc[0][0])[i] = 0ull;
     if constexpr (KIND == 2) {
         // the E window's clean samples 2T[n] (both LTF slots hold T): one spectrum per block
@@ -237,6 +259,7 @@ __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_
         const int64_t grp = tail ? R * B + tw / S : w;
         const int sub = tail ? tw % S : 0, ns = tail ? S : 1;
         __syncthreads();                                   // every wave is done with the last group
+        PK_STAMP(0);                                       // item-top barrier (waiting for the other waves)
         // group-invariant addresses are re-derived from the thread index here, not held across the SNR
         // loop (they would be the only values spilled)
         int t = tid;
@@ -286,7 +309,7 @@ __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_
                 // warm L2 with the next item's group (64 rows x 1 KB: one 4-byte LDS-DMA read per 128-B
                 // line, into a dummy LDS word), so the next prologue's loads hit L2 instead of HBM (not when
                 // the launch builds its own batch: those rows are written by the next item itself)
-                if (nx < n_items && !own_tx) {
+                if (nx < n_items && !own_tx && !WLATE) {
                     const int64_t ng = nx < R * B ? nx : R * B + (nx - R * B) / S;
 #pragma unroll
                     for (int i = 0; i < 8; ++i) {
@@ -315,7 +338,9 @@ __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_
                 else chan_pairs<1>(h, &fce[0][fr]);
             }
         }
+        PK_STAMP(1);                                       // prologue work
         __syncthreads();
+        PK_STAMP(2);                                       // prologue barrier
         if constexpr (FADE) {
             // faded spectra: C <- H' C for both data symbols, and fce <- H' FFT(2T) (the frame's LS reference);
             // one (pair, frame) per thread and step, so each H' is read and overwritten by one thread
@@ -332,10 +357,31 @@ __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_
             }
             __syncthreads();
         }
+        PK_STAMP(3);                                       // Rayleigh: faded spectra
         const int64_t fl = grp * PK_FRAMES + lane;
         const bool valid = fl < a.n_frames;
         const uint64_t f = a.first_frame + (uint64_t)fl;
         for (int q = wv + 4 * sub; q < a.n_snr; q += 4 * ns) {
+            // LS AWGN: wave 2 warms L2 with the next item's rows at the start of its last SNR iteration, one
+            // iteration before the next prologue reads them (warmed in the prologue, a whole item earlier, most
+            // lines were evicted again: 64 blocks per XCD warm 4 MB into its 4 MB L2)
+            if constexpr (WLATE) {
+                if (wv == 2 && q + 4 * ns >= a.n_snr) {
+                    const int nx = __builtin_amdgcn_readfirstlane(next_item);
+                    using KArgsW = const __attribute__((address_space(4))) RxArgs;
+                    KArgsW *apw = (KArgsW *)__builtin_amdgcn_kernarg_segment_ptr();
+                    if (nx < n_items && apw->own.n_sym == 0) {
+                        const int64_t ng = nx < R * B ? nx : R * B + (nx - R * B) / S;
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) {
+                            const int line = lane + 64 * i;                    // 0..511
+                            const float2 *p = a.tx + (int64_t)(16 + (line >> 3)) * a.pitch + ng * PK_SYMS + (line & 7) * 16;
+                            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)p,
+                                                             (__attribute__((address_space(3))) void *)pf_dummy, 4, 0, 0);
+                        }
+                    }
+                }
+            }
             uint32_t flo = (uint32_t)f, fhi = (uint32_t)(f >> 32);
             opaque(flo); opaque(fhi);
             const float sigma = a.sigma[q];
@@ -540,14 +586,35 @@ __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_
             frame_metrics(acc, KIND == 2 ? 4.0f * evm : evm, be, ax);
             flush_lanes(acc, valid, sacc[q]);
         }
+        PK_STAMP(4);                                       // SNR loop
     }
     block_flush(a, sacc);
+    PK_STAMP(5);                                           // block flush
+#ifdef OFDM_PACK_STAMPS
+    if (lane == 0)
+        for (int k = 0; k < 6; ++k) atomicAdd(&g_pack_stamps[wv][k], st_acc[k]);
+#endif
 }
 
 template <int KIND, int CONV, int CHAN = OFDM_CHAN_AWGN>
 static void launch_pack_t(hipStream_t st, const RxArgs &a, bool dump, unsigned grid) {
     if (dump) hipLaunchKernelGGL((rx_pack_kernel<KIND, CONV, CHAN, true>), dim3(grid), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((rx_pack_kernel<KIND, CONV, CHAN, false>), dim3(grid), dim3(256), 0, st, a);
+#ifdef OFDM_PACK_STAMPS
+    // cumulative over the process's launches: wave 0 (clean spectra) and wave 2 (Tx / warm-up) roles
+    unsigned long long hs[4][8];
+    if (hipStreamSynchronize(st) == hipSuccess && hipMemcpyFromSymbol(hs, HIP_SYMBOL(g_pack_stamps), sizeof hs) == hipSuccess) {
+        static const char *names[6] = {"item-top barrier", "prologue work", "prologue barrier", "faded spectra",
+                                       "SNR loop", "block flush"};
+        for (int w : {0, 2}) {
+            double tot = 0;
+            for (int k = 0; k < 6; ++k) tot += (double)hs[w][k];
+            fprintf(stderr, "pack stamp wave %d:", w);
+            for (int k = 0; k < 6; ++k) fprintf(stderr, " %s %.2f%%;", names[k], 100.0 * (double)hs[w][k] / tot);
+            fprintf(stderr, "\n");
+        }
+    }
+#endif
 }
 
 template <const void *(*K)()>

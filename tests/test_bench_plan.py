@@ -142,6 +142,24 @@ def test_kernel_build_id_tracks_code_bytes(pkg, tmp_path):
     assert codeobj.workload_build_id(mod, "c5") == codeobj.workload_build_id(lib, "c5")
 
 
+def test_kernel_build_id_ignores_code_placement(pkg, tmp_path):
+    """The descriptor's code-entry offset (bytes 16-23 of the .kd) moves when another kernel of the library
+    changes size: the id ignores it, while any other descriptor byte (register / LDS settings) counts."""
+    from ofdm_amd import abi, codeobj
+    lib = abi.library_file()
+    syms = codeobj.kernel_symbols(lib)
+    kd = next(n for n in syms if "rx_pack_kernelILi2ELi0ELi0ELb0E" in n and n.endswith(".kd"))
+    blob = bytes(lib.read_bytes())
+    at = blob.find(syms[kd])
+    assert at > 0 and blob.count(syms[kd]) == 1
+    for off, same in ((17, True), (20, True), (0, False), (48, False)):
+        b = bytearray(blob)
+        b[at + off] ^= 0x01
+        mod = tmp_path / f"lib_kd_{off}.so"
+        mod.write_bytes(bytes(b))
+        assert (codeobj.workload_build_id(mod, "c3") == codeobj.workload_build_id(lib, "c3")) == same, off
+
+
 def test_host_cpu_share_is_derived(monkeypatch):
     b = _bench()
     monkeypatch.setattr(b, "_cgroup_cpu_quota", lambda: (3.0, "cgroup v2 cpu.max 300000/100000"))
