@@ -137,7 +137,7 @@ def gen_genie(R: RefLib, frames: int = 20000, snrs=(0.0, 2.0, 4.0, 6.0)):
 
 MC_SNRS = list(range(0, 17)) + [18, 20, 22, 24, 26, 28, 30]
 MC_DEEP_SNRS = (11, 12, 13, 14, 15)     # the BER waterfall, where the curve is set by rare sync failures
-MC_DEEP_SCALE = {13: 4, 14: 4}          # x --mc-deep-trials where the 1e-3.5 / 1e-4 crossings are pinned
+MC_DEEP_SCALE = {13: 4, 14: 4, 15: 4}   # x --mc-deep-trials where the 1e-3.5 .. 1e-5 crossings are pinned
 MC_DEEP_JOB = 25_000                    # trials per deep job (seeded by job index: independent of --procs)
 
 
@@ -204,7 +204,7 @@ def gen_mc(trials: int, procs: int, deep_trials: int):
 
 def main():
     ap = argparse.ArgumentParser()
-    # the defaults reproduce the committed ref_mc_curve.json (48000 trials/point, 1e6 at 11, 12, 15 dB, 4e6 at 13, 14)
+    # the defaults reproduce the committed ref_mc_curve.json (48000 trials/point, 1e6 at 11, 12 dB, 4e6 at 13, 14, 15)
     ap.add_argument("--mc-trials", type=int, default=48000)
     ap.add_argument("--mc-deep-trials", type=int, default=1_000_000)
     ap.add_argument("--procs", type=int, default=8)

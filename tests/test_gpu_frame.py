@@ -247,11 +247,11 @@ def test_reference_ber_curve_within_tenth_db(engine, pkg):
     """north_star: reproduce the reference BER-vs-SNR curve within +-0.1 dB, down the waterfall.
 
     Reference: the compiled OFDM.c's own trial loop (ref_mc_curve.json; 48000 trials/point, 1e6 at
-    11, 12, 15 dB and 4e6 at 13, 14 dB where the curve is set by rare failed frames, OFDM.c:752-761, BER
+    11, 12 dB and 4e6 at 13, 14, 15 dB where the curve is set by rare failed frames, OFDM.c:752-761, BER
     OFDM.c:1152-1161, loop OFDM.c:1195-1222).  GPU: 1e7 trials/point in 50 batches.  The SNR where log10
     BER crosses each level (log-linear interpolation between the 1-dB points) must agree within 0.1 dB at
-    every level from 10^-1 down to the deepest one whose two bracketing reference points each hold >= 100
-    trials with errors (10^-4).  Point-wise, the two means agree within 5 frame-clustered standard errors: the reference's from
+    every level from 10^-1 down to 10^-5 (the deepest whose crossing lies inside the 15-dB fixture; its
+    bracketing points 14 / 15 dB hold 2513 / 309 reference trials with errors, >= 100 required).  Point-wise, the two means agree within 5 frame-clustered standard errors: the reference's from
     its per-trial BER variance (a failed sync costs ~half the bits at once) plus a pseudo-count of one
     failed frame, the GPU's from the spread of its 50 batches."""
     rows = [r for r in json.loads((GOLDEN / "ref_mc_curve.json").read_text())["rows"] if r["snr_db"] <= 15]
@@ -265,7 +265,7 @@ def test_reference_ber_curve_within_tenth_db(engine, pkg):
     se_gpu = bb.std(axis=0, ddof=1) / np.sqrt(K)
     se_ref = np.sqrt((np.array([r["ber_trial_var"] for r in rows]) * n_ref + 0.25) / n_ref ** 2)
     checked = []
-    for level in np.arange(-1.0, -6.01, -0.5):
+    for level in np.arange(-1.0, -5.01, -0.5):
         s_ref, s_gpu = _snr_at(snr, ref, level), _snr_at(snr, ber, level)
         if s_ref is None:
             break
@@ -277,7 +277,7 @@ def test_reference_ber_curve_within_tenth_db(engine, pkg):
               f"(reference failed frames {fails[i - 1]} / {fails[i]})")
         assert abs(s_ref - s_gpu) < 0.1, (level, s_ref, s_gpu)
         checked.append(level)
-    assert min(checked) <= -3.5, checked                # the waterfall, not just its shoulder
+    assert min(checked) <= -5.0, checked                # the waterfall down to 1e-5, not just its shoulder
     for s, b, r, eg, er, fe in zip(snr, ber, ref, se_gpu, se_ref, ferr):
         z = (b - r) / np.hypot(eg, er)
         print(f"{s:5.1f} dB  BER GPU {b:.4e}  reference {r:.4e}  z {z:+.2f}  GPU frame errors {fe}")
