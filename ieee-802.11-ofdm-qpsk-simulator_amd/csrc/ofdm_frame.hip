@@ -1099,7 +1099,10 @@ static int run_frame_chunk(Ctx *c, FrameArgs &a) {
     a.im_period = a.ext ? (1 << 30) : a.wave_len / FR_REPS;
     a.im_magic = (uint32_t)((((uint64_t)1 << 32) + (uint64_t)a.im_period - 1) / (uint64_t)a.im_period);
     a.imt_len = (a.ext ? a.cap_len : a.im_period) + IMT_EXT;
-    const size_t lds = frame_lds_bytes(a.cap_len, a.n_data, a.n_snr, a.imt_len, a.word_stats);
+#ifndef FRAME_LDS_PAD
+#define FRAME_LDS_PAD 0     // A/B only: unused LDS per block, to measure K4b at lower occupancy
+#endif
+    const size_t lds = frame_lds_bytes(a.cap_len, a.n_data, a.n_snr, a.imt_len, a.word_stats) + FRAME_LDS_PAD;
     a.fr_in_cap = fr_in_capture(a.cap_len, a.n_data);
     if (!c->d_work) HIPOK(hipMalloc(&c->d_work, 256));
     a.work = (unsigned long long *)c->d_work;
