@@ -34,7 +34,8 @@ CFLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-fno-slp-vecto
 # with the prologue's Tx builds, max-ILP spills them at their 168-VGPR budget.
 SOURCE_FLAGS = {"ofdm_symbol.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
                 "ofdm_rxpack.hip": os.environ.get("OFDM_RXPACK_FLAGS", "-mllvm -amdgpu-sched-strategy=max-ilp").split(),
-                "ofdm_rxpack_ideal.hip": os.environ.get("OFDM_RXPACK_IDEAL_FLAGS", "").split()}
+                "ofdm_rxpack_ideal.hip": os.environ.get("OFDM_RXPACK_IDEAL_FLAGS", "").split(),
+                "ofdm_frame.hip": os.environ.get("OFDM_FRAME_FLAGS", "").split()}
 
 
 # Kernels whose parity-dump variants (last template argument `true`) are allowed to spill: they
