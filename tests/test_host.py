@@ -66,6 +66,25 @@ def test_errors_without_context(pkg):
     assert rc == -1
 
 
+def test_every_entry_point_rejects_a_null_context(pkg):
+    """Each entry point that takes an ofdm_ctx returns OFDM_E_ARG with a message for a NULL context (all
+    other arguments zero / NULL), before any HIP call: an error code, never a crash or exit()."""
+    import ctypes as C
+    from ofdm_amd import abi
+    lib = pkg.load_library()
+    checked = 0
+    for name, (_, argtypes) in abi._SIGS.items():
+        if not argtypes or argtypes[0] is not abi._V or name == "ofdm_ctx_destroy":   # destroy(NULL) is a no-op
+            continue
+        args = [None if t in (abi._V, C.c_char_p) or t.__name__.startswith("LP_") else 0 for t in argtypes]
+        rc = getattr(lib, name)(*args)
+        assert rc == -1, (name, rc)
+        assert lib.ofdm_last_error(), name
+        checked += 1
+    assert checked == len([n for n, (_, t) in abi._SIGS.items() if t and t[0] is abi._V]) - 1, checked
+    assert lib.ofdm_ctx_destroy(None) == 0
+
+
 def test_tx_bytes(pkg):
     import ctypes as C
     lib = pkg.load_library()
