@@ -260,6 +260,14 @@ __device__ __forceinline__ void dif_stage1(float2 (&x)[64]) { dif_bfly<INV, 64, 
 template <bool INV, int R>
 __device__ __forceinline__ void dif_sub16(float2 (&x)[64]) { dif4<INV, 16, 16 * R>(x); }
 
+// this lane's index re-derived where it is used (v_mbcnt, volatile: never hoisted), so that a kernel at a
+// tight register budget does not hold the work-item id in a VGPR across its long loops
+__device__ __forceinline__ int lane_fresh() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
 #ifndef OFDM_NO_SCHED_FENCE
 __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
 #else

@@ -272,17 +272,17 @@ __device__ __forceinline__ int slot_term(const unsigned long long *s, int k, uns
     }
 }
 
-template <int S>   // slots per SNR point in the block's LDS accumulators (>= 5)
-__device__ __forceinline__ void block_flush(const RxArgs &a, unsigned long long (*sacc)[S]) {
+template <int S>   // slots per SNR point in the block's LDS accumulators (>= 5); tid = threadIdx.x
+__device__ __forceinline__ void block_flush(const RxArgs &a, unsigned long long (*sacc)[S], int tid) {
     __syncthreads();
-    for (int i = threadIdx.x; i < a.n_snr * 7; i += blockDim.x) {
+    for (int i = tid; i < a.n_snr * 7; i += blockDim.x) {
         const int q = i / 7, k = i % 7;
         unsigned long long v;
         const int ci = slot_term(sacc[q], k, v);
         if (v) atomicAdd(&a.counters[q * OFDM_NCOUNTERS + ci], v);
     }
     if (blockIdx.x == 0) {
-        for (int q = threadIdx.x; q < a.n_snr; q += blockDim.x) {
+        for (int q = tid; q < a.n_snr; q += blockDim.x) {
             unsigned long long *c = a.counters + q * OFDM_NCOUNTERS;
             atomicAdd(&c[OFDM_C_FRAMES], (unsigned long long)a.n_frames);
             atomicAdd(&c[OFDM_C_SYMBOLS], (unsigned long long)(2 * a.n_frames));
@@ -290,6 +290,10 @@ __device__ __forceinline__ void block_flush(const RxArgs &a, unsigned long long 
             atomicAdd(&c[OFDM_C_EVM_TERMS], (unsigned long long)(96 * a.n_frames));
         }
     }
+}
+template <int S>
+__device__ __forceinline__ void block_flush(const RxArgs &a, unsigned long long (*sacc)[S]) {
+    block_flush(a, sacc, (int)threadIdx.x);
 }
 
 

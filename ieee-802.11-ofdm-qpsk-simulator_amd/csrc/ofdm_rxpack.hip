@@ -19,8 +19,14 @@
 #include "ofdm_internal.h"
 #include "ofdm_rxcommon.h"
 
-#ifndef OFDM_RX_PACK_WAVES          // waves per SIMD the LS receiver is register-budgeted for (220 VGPRs)
-#define OFDM_RX_PACK_WAVES 2
+#ifndef OFDM_PACK_SPLITD            // LS AWGN: data windows as two 32-point real FFTs (see the SNR loop)
+#define OFDM_PACK_SPLITD 0
+#endif
+#ifndef OFDM_RX_PACK_WAVES          // waves per SIMD the LS receiver is register-budgeted for
+#define OFDM_RX_PACK_WAVES (OFDM_PACK_SPLITD ? 3 : 2)
+#endif
+#ifndef OFDM_PACK_SPLIT_PF          // split loop: bin-pair LDS operands loaded this many pairs ahead
+#define OFDM_PACK_SPLIT_PF 1
 #endif
 #ifndef OFDM_RX_PACK_IDEAL_WAVES    // the ideal-CSI receiver (no LTF spectrum) fits 168 VGPRs / 53 KB LDS
 #define OFDM_RX_PACK_IDEAL_WAVES 3
@@ -36,6 +42,7 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) const f4v lcf4;
 typedef unsigned int u2v __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) const u2v lcu2;
+typedef __attribute__((address_space(3))) const uint32_t lcu1;
 typedef __attribute__((address_space(3))) f2v lf2;
 
 // the LTF noise spectrum E'[k] of the odd-k pairs waits in LDS (per wave) until the odd sub-blocks are
@@ -83,6 +90,9 @@ __device__ __forceinline__ void chan_pairs(const float2 (&h)[4], float4 *col) {
 
 // Group prologue: clean spectrum of symbol `s` (window rows 16..79 of the Tx batch, times (-1)^n for
 // fft(), OFDM.c:314-318) -> the 24 bin pairs (C[k], C[64 - k]) of spec[p][half][frame].
+// EARLY: each sub-block's pairs are stored as soon as they are final (sub-block 0, 2, then 1 + 3), which
+// lowers the register peak of the 168-VGPR split receiver's prologue.
+template <bool EARLY = false>
 __device__ __forceinline__ void clean_spectrum(const RxArgs &a, int64_t s, float4 *spec_col /* &spec[0][half][f] */) {
     gcf2 *src = (gcf2 *)(a.tx + 16 * a.pitch + s);
     int P = (int)a.pitch;
@@ -100,13 +110,26 @@ __device__ __forceinline__ void clean_spectrum(const RxArgs &a, int64_t s, float
         static_for<0, 4>([&](auto ic) { dif_stage1<false, 4 * g + decltype(ic)::value>(x); });
         sched_fence();
     });
-    static_for<0, 4>([&](auto rc) { dif_sub16<false, decltype(rc)::value>(x); });
-    static_for<0, PACK_PAIRS>([&](auto pc) {
+    auto store = [&](auto pc) {
         constexpr int p = decltype(pc)::value;
         constexpr int k = pair_bin(p);
         const float2 c0 = x[digit_rev4(k)], c1 = x[digit_rev4(64 - k)];
         spec_col[p * 2 * PK_FRAMES] = make_float4(c0.x, c0.y, c1.x, c1.y);
-    });
+    };
+    if constexpr (EARLY) {
+        dif_sub16<false, 0>(x);
+        static_for<0, 6>(store);
+        sched_fence();
+        dif_sub16<false, 2>(x);
+        static_for<6, 13>(store);
+        sched_fence();
+        dif_sub16<false, 1>(x);
+        dif_sub16<false, 3>(x);
+        static_for<13, PACK_PAIRS>(store);
+    } else {
+        static_for<0, 4>([&](auto rc) { dif_sub16<false, decltype(rc)::value>(x); });
+        static_for<0, PACK_PAIRS>(store);
+    }
 }
 
 // Per-bin demap of one data symbol at one bin: u = Z / g with g > 0 (KIND 0: g = 1, KIND 2: g = 2r),
@@ -184,11 +207,20 @@ static __device__ unsigned long long g_pack_stamps[4][8];
 // CHAN (KIND 2 only): OFDM_CHAN_RAYLEIGH4 applies each frame's 4-tap channel to its clean spectra in the
 // group prologue (chan_bin): it does not depend on the SNR point, and the real noise is added after the
 // channel (OFDM.c:651 order), so the SNR loop is the AWGN loop with a per-frame E spectrum `fce`.
+#ifndef OFDM_RX_PACK_FADE_WAVES     // the Rayleigh LS receiver (72 KB of LDS: two blocks per CU)
+#define OFDM_RX_PACK_FADE_WAVES 2
+#endif
 template <int KIND, int CONV, int CHAN, bool DUMP>
-__global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_IDEAL_WAVES) void rx_pack_kernel(RxArgs a) {
+__global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFDM_RX_PACK_FADE_WAVES : OFDM_RX_PACK_WAVES)
+                                            : OFDM_RX_PACK_IDEAL_WAVES) void rx_pack_kernel(RxArgs a) {
     constexpr bool FADE = CHAN == OFDM_CHAN_RAYLEIGH4;
     static_assert(!FADE || KIND == 2, "the packed Rayleigh receiver is the LS one");
+    // LS AWGN, split data windows: D0 and D1 each through a 32-point FFT of its even/odd samples (the LTF
+    // pair's transform), demapped pass by pass, instead of d0 + j d1 through one 64-point FFT: the E
+    // spectrum (48 VGPRs) is then live beside 64 VGPRs of transform instead of 128
+    constexpr bool SPLIT = KIND == 2 && !FADE && OFDM_PACK_SPLITD;
     constexpr bool EEL = KIND == 2 && EE_LDS_N > 0;
+    static_assert(!(SPLIT && EEL), "the split loop keeps the whole E spectrum in VGPRs");
 #ifndef OFDM_NO_PACK_WARM_LATE
     constexpr bool WLATE = KIND == 2 && !FADE;      // where the next item's L2 warm-up is issued (see the SNR loop)
 #else
@@ -262,7 +294,7 @@ __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_
         PK_STAMP(0);                                       // item-top barrier (waiting for the other waves)
         // group-invariant addresses are re-derived from the thread index here, not held across the SNR
         // loop (they would be the only values spilled)
-        int t = tid;
+        int t = SPLIT ? (wv << 6) + lane_fresh() : tid;
         opaque(t);
         // kernel arguments read where used through an opaque kernarg pointer: hoisted, the 40 words of each
         // TxArgs would be held in SGPRs across the item loop and spill
@@ -289,7 +321,7 @@ __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_
 #else
         if (t < PK_SYMS) {
 #endif
-            clean_spectrum(a, grp * PK_SYMS + t, &spec[0][t & 1][t >> 1]);
+            clean_spectrum<SPLIT>(a, grp * PK_SYMS + t, &spec[0][t & 1][t >> 1]);
         } else {
             const int j = t - PK_SYMS;
             const uint32_t *src = a.bits + 7 * a.pitch + grp * PK_SYMS + j;
@@ -358,7 +390,7 @@ __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_
             __syncthreads();
         }
         PK_STAMP(3);                                       // Rayleigh: faded spectra
-        const int64_t fl = grp * PK_FRAMES + lane;
+        const int64_t fl = grp * PK_FRAMES + (SPLIT ? lane_fresh() : lane);
         const bool valid = fl < a.n_frames;
         const uint64_t f = a.first_frame + (uint64_t)fl;
         for (int q = wv + 4 * sub; q < a.n_snr; q += 4 * ns) {
@@ -372,9 +404,10 @@ __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_
                     KArgsW *apw = (KArgsW *)__builtin_amdgcn_kernarg_segment_ptr();
                     if (nx < n_items && apw->own.n_sym == 0) {
                         const int64_t ng = nx < R * B ? nx : R * B + (nx - R * B) / S;
+                        const int ln = SPLIT ? lane_fresh() : lane;     // split: nothing lane-derived held
 #pragma unroll
                         for (int i = 0; i < 8; ++i) {
-                            const int line = lane + 64 * i;                    // 0..511
+                            const int line = ln + 64 * i;                      // 0..511
                             const float2 *p = a.tx + (int64_t)(16 + (line >> 3)) * a.pitch + ng * PK_SYMS + (line & 7) * 16;
                             __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)p,
                                                              (__attribute__((address_space(3))) void *)pf_dummy, 4, 0, 0);
@@ -437,6 +470,108 @@ __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_
                 });
                 sched_fence();
             }
+            if constexpr (SPLIT) {
+                // ---- data window D (D0 at t = 336 + n, Philox block 84 + n/4; D1 at t = 416 + n, block 104 + n/4)
+                // packed as z[m] = e'[2m] + j e'[2m+1], e'[n] = (-1)^n d[n], through the LTF pair's 32-point
+                // transform; per bin pair 2 N[k] = (Z[k] + conj Z[-k]) - j W64^k (Z[k] - conj Z[-k]), then the
+                // clean spectrum, the LS estimate (S and 1/|S|^2 recomputed in each pass), ZF and the demap
+                const float K = noise_k(sigma);
+                float evm = 0.f;
+                uint32_t em = 0u, be = 0u, ax = 0u, t = 0u;
+                uint32_t sm;
+                asm volatile("v_mov_b32 %0, 0x80000000" : "=v"(sm));
+                const int ln = lane_fresh();
+                lcf4 *sp = (lcf4 *)&spec[0][0][ln];
+                lcu1 *tw = (lcu1 *)&truth[0][2 * ln];
+                opaque(sp); opaque(tw);
+                static_for<0, 2>([&](auto Dc) {
+                    constexpr int D = decltype(Dc)::value;
+                    static_for<0, 4>([&](auto ic) {
+                        constexpr int i = decltype(ic)::value;
+                        uint32_t tg = 84u + 20u * D + 2 * i;
+                        opaque(tg);
+                        static_for<0, 2>([&](auto hc) {
+                            constexpr int h = decltype(hc)::value;
+                            const Noise4 lo = pack_noise(hd, tg + h, PKEYS, K);
+                            const Noise4 hi = pack_noise(hd, tg + 8 + h, PKEYS, K);
+                            constexpr int m = 4 * i + 2 * h;
+                            z[m] = make_float2(lo.r0 * lo.c0, -(lo.r0 * lo.s0));
+                            z[m + 1] = make_float2(lo.r1 * lo.c1, -(lo.r1 * lo.s1));
+                            z[m + 16] = make_float2(hi.r0 * hi.c0, -(hi.r0 * hi.s0));
+                            z[m + 17] = make_float2(hi.r1 * hi.c1, -(hi.r1 * hi.s1));
+                        });
+                        static_for<0, 4>([&](auto jc) {
+                            constexpr int j = 4 * i + decltype(jc)::value;
+                            const float2 u = z[j], v = z[j + 16];
+                            z[j] = cadd(u, v);
+                            z[j + 16] = twiddle<2 * j, false>(csub(u, v));
+                        });
+                        sched_fence();
+                    });
+                    float2 *deq = nullptr;
+                    uint32_t *dbit = nullptr;
+                    if constexpr (DUMP) {
+                        if (valid) {
+                            const int64_t r0 = ((int64_t)q * a.dump_frames + fl) * 2 + D;
+                            deq = a.dump_eq + r0 * 48;
+                            dbit = a.dump_bits + r0 * 3;
+                        }
+                    }
+                    uint32_t db[3] = {0u, 0u, 0u};
+                    constexpr int PF = OFDM_PACK_SPLIT_PF;
+                    f4v pcs[PF + 1];
+                    float4 pe4[PF + 1];
+                    auto load_pair = [&](auto pc) {
+                        constexpr int p = decltype(pc)::value;
+                        if constexpr (p < PACK_PAIRS) {
+                            pcs[p % (PF + 1)] = sp[(p * 2 + D) * PK_FRAMES];
+                            pe4[p % (PF + 1)] = ce[p];
+                        }
+                    };
+                    static_for<0, PF + 1>(load_pair);
+                    auto pair = [&](auto pc) {
+                        constexpr int p = decltype(pc)::value;
+                        constexpr int k = pair_bin(p), k2 = 64 - k;
+                        if constexpr ((p & 7) == 0) t = tw[(p >> 3) * PK_SYMS + D];
+                        const f4v c = pcs[p % (PF + 1)];
+                        const float4 e4 = pe4[p % (PF + 1)];
+                        load_pair(std::integral_constant<int, p + PF + 1>{});
+                        const float2 P = z[pos32(k)], Qv = z[pos32(32 - k)];
+                        const float2 F = make_float2(P.x + Qv.x, P.y - Qv.y);
+                        const float2 H = twiddle<k, false>(make_float2(P.x - Qv.x, P.y + Qv.y));
+                        const float2 V = make_float2(F.x + H.y, F.y - H.x);          // 2 N[k]
+                        const float2 yk = make_float2(fmaf(0.5f, V.x, c.x), fmaf(0.5f, V.y, c.y));
+                        const float2 ym = make_float2(fmaf(0.5f, V.x, c.z), fmaf(-0.5f, V.y, c.w));
+                        const float2 Sk = make_float2(fmaf(0.5f, ee[p].x, e4.x), fmaf(0.5f, ee[p].y, e4.y));
+                        const float2 Sm = make_float2(fmaf(0.5f, ee[p].x, e4.z), fmaf(-0.5f, ee[p].y, e4.w));
+                        const float rk = __builtin_amdgcn_rcpf(fmaf(Sk.x, Sk.x, Sk.y * Sk.y));
+                        const float rm = __builtin_amdgcn_rcpf(fmaf(Sm.x, Sm.x, Sm.y * Sm.y));
+                        const float2 uk = cscale(cmulc(yk, Sk), (float)ltf_sign(k));
+                        const float2 um = cscale(cmulc(ym, Sm), (float)ltf_sign(k2));
+                        demap_bin<2, DUMP>(uk, rk, t, sm, evm, em, data_index(k), deq, db);
+                        demap_bin<2, DUMP>(um, rm, t, sm, evm, em, data_index(k2), deq, db);
+                        if constexpr ((p & 7) == 7) {
+                            ax += __popc(em);
+                            be += __popc(em & 0x55555555u) + __popc((em ^ (em >> 1)) & 0x55555555u);
+                            em = 0u;
+                        }
+                        opaque(evm);
+                        if constexpr ((p & 1) == 1) sched_fence();
+                    };
+                    dif4<false, 16, 0>(z);
+                    static_for<0, 13>(pair);      // even k: the first 16-point sub-transform
+                    sched_fence();
+                    dif4<false, 16, 16>(z);
+                    static_for<13, PACK_PAIRS>(pair);
+                    if constexpr (DUMP) {
+                        if (dbit) { dbit[0] = db[0]; dbit[1] = db[1]; dbit[2] = db[2]; }
+                    }
+                    sched_fence();
+                });
+                FrameAcc acc;
+                frame_metrics(acc, 4.0f * evm, be, ax);
+                flush_lanes(acc, valid, sacc[q]);
+            } else {
             // ---- data windows: x[n] = (-1)^n (d0[n] + j d1[n]) fused with the first radix-4 stage.
             // Gaussian t of the frame's stream is sample t of the frame timeline: D0 at
             // t = 336 + n (Philox block 84 + n/4), D1 at t = 416 + n (block 104 + n/4).
@@ -585,10 +720,11 @@ __global__ __launch_bounds__(256, KIND == 2 ? OFDM_RX_PACK_WAVES : OFDM_RX_PACK_
             FrameAcc acc;
             frame_metrics(acc, KIND == 2 ? 4.0f * evm : evm, be, ax);
             flush_lanes(acc, valid, sacc[q]);
+            }   // !SPLIT
         }
-        PK_STAMP(4);                                       // SNR loop
+        PK_STAMP(4);                                     // SNR loop
     }
-    block_flush(a, sacc);
+    block_flush(a, sacc, SPLIT ? (wv << 6) + lane_fresh() : tid);
     PK_STAMP(5);                                           // block flush
 #ifdef OFDM_PACK_STAMPS
     if (lane == 0)
