@@ -19,6 +19,7 @@
 #include "ofdm_ctx.h"
 #include "ofdm_rxcommon.h"
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -57,6 +58,7 @@ struct FrameArgs {
     int64_t n_trials;
     int32_t n_snr, q_base;
     int32_t cap_len, float_cfo, matlab, fixed_start, noise, wave_len, n_data, word_stats;
+    int32_t no_lazy;                // 1: evaluate every capture in full (OFDM_FRAME_NO_LAZY, the lazy path's test)
     int32_t fr_in_cap;              // fr[] inside the capture region (fr_in_capture)
     int32_t imt_len, im_period;     // LDS table of the capture's imaginary parts: length, index period
     uint32_t im_magic;              // ceil(2^32 / im_period): x mod im_period by one multiply-high (x < 2^14)
@@ -383,6 +385,67 @@ __device__ __forceinline__ void lds_readn(const float *p, int s, float (&x)[N]) 
     if constexpr (!ODD) x[N - 1] = p[s + N - 1];
 }
 
+#ifndef FRAME_LAZY
+#define FRAME_LAZY 1        // lazy capture + detection (see frame_sync_kernel; A/B: +5.3 %, profiles/r03/ab_n/)
+#endif
+#ifndef FRAME_LAZY_C0
+#define FRAME_LAZY_C0 31    // round-0 positions per lane when lazy (two 16-position batches)
+#endif
+
+// Capture Philox blocks bs..be (block b = waveform samples 4b..4b+3; b0 = the capture's first block) into the
+// wave's region: the real parts of the clean waveform plus real AWGN (OFDM.c:622-655, D7).
+template <typename A>
+__device__ __forceinline__ void capture_blocks(const A &a, float *rbase, int b0, int bs, int be, int lane, uint32_t t_lo,
+                                               uint32_t t_hi, uint32_t qs, float sigma) {
+    const PhiloxHead hd = philox_head(t_lo, t_hi, STREAM_NOISE | qs, a.k1);
+    const float Ksig = noise_k(sigma);
+#ifndef FRAME_CAP_SKEYS
+    // round keys in VGPRs: each round's two v_bitop3_b32 issue at the fast rate (an SGPR operand makes
+    // them slow-class); 20 VGPRs for the capture loop only
+    PhiloxKeysV vk;
+    vk.init(a.k0, a.k1);
+#endif
+    // Gaussian k of the trial's stream goes to waveform sample k (as if Transmission_Over_Air had drawn
+    // the whole waveform); only the captured samples are ever evaluated.  The waveform is FR_REPS
+    // copies of one filtered frame (OFDM.c:607-612): sample k is sample k mod nfilt of the first copy
+    // (7.8 KB, L1-resident).  bm = the block's index within the copy.
+    const uint32_t pb = (uint32_t)(a.wave_len / (4 * FR_REPS)), nb_wave = (uint32_t)(a.wave_len / 4);
+    uint32_t bm = (uint32_t)(bs + lane) % pb;
+#ifndef FRAME_CAP_U
+#define FRAME_CAP_U 6   // Philox blocks per lane per pass: 12 of a reference capture in 2 passes (A/B: +0.8 % over 3)
+#endif
+    for (int bb = bs + lane; bb <= be; bb += FRAME_CAP_U * 64) {
+        float4 v[FRAME_CAP_U];
+#pragma unroll
+        for (int u = 0; u < FRAME_CAP_U; ++u) {
+            const int b = bb + 64 * u;
+            const float4 *s4 = reinterpret_cast<const float4 *>(a.wave + 4 * bm);
+            const bool in = b <= be && (uint32_t)b < nb_wave;
+            const float4 lo = in ? s4[0] : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 hi = in ? s4[1] : make_float4(0.f, 0.f, 0.f, 0.f);
+            v[u] = make_float4(lo.x, lo.z, hi.x, hi.z);
+            bm = bm + 64 >= pb ? bm + 64 - pb : bm + 64;           // (bm + 64) mod pb (pb > 64)
+        }
+#pragma unroll
+        for (int u = 0; u < FRAME_CAP_U; ++u) {
+            const int b = bb + 64 * u;
+            if (b > be) break;
+            float4 w = v[u];
+            if (a.noise == OFDM_NOISE_REAL) {   // real-only (D7): sigma z = sqrt(K log2 u1) (cos | sin)
+#ifndef FRAME_CAP_SKEYS
+                const Noise4 nz = noise4_of(philox10_c2(hd, (uint32_t)b, vk), Ksig);
+#else
+                const Noise4 nz = noise4_of(philox10_c2(hd, (uint32_t)b, a.k0, a.k1), Ksig);
+#endif
+                w.x = fmaf(nz.r0, nz.c0, w.x); w.y = fmaf(nz.r0, nz.s0, w.y);
+                w.z = fmaf(nz.r1, nz.c1, w.z); w.w = fmaf(nz.r1, nz.s1, w.w);
+            }
+            // samples of the block outside [0, L) land in the region's slack, never read as capture
+            *reinterpret_cast<float4 *>(rbase + 4 * (b - b0)) = w;
+        }
+    }
+}
+
 #ifndef FRAME_SYNC_MINW
 #define FRAME_SYNC_MINW 3   // waves per SIMD the VGPR budget targets (LDS holds 3 blocks of 4 waves per CU)
 #endif
@@ -411,10 +474,22 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
     unsigned long long stamp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long stamp_t = __builtin_amdgcn_s_memtime();
 #endif
-    // detection geometry: R rounds of 64 lanes x chunk positions (chunk odd: the lanes' LDS reads fall in
-    // distinct banks); one round for the reference capture (chunk 47)
+    // detection geometry: R rounds of 64 lanes, round 0 c0 positions per lane over [0, B1 = 64 c0), round 1 c1
+    // per lane from B1 (chunks odd: the lanes' LDS reads fall in distinct banks)
+#if FRAME_LAZY
+    // Lazy: round 0 covers the first 64 FRAME_LAZY_C0 positions (the reference capture: 1984 of 2961), and only
+    // the capture samples round 0 reads are generated before it; when round 0 alone decides Packet_Selection and
+    // the matched filter reads inside that part, the rest of the capture and round 1 are skipped (same
+    // packet_idx, same frame: see the selection below).
+    const int c0 = Lc > 64 * FRAME_LAZY_C0 ? FRAME_LAZY_C0 : (((Lc + 63) / 64) | 1);
+    const int B1 = 64 * c0;
+    const int R = Lc > B1 ? 2 : 1;
+    const int c1 = R == 2 ? (((Lc - B1 + 63) / 64) | 1) : c0;
+#else
+    // one round for the reference capture (chunk 47)
     const int R = (Lc + 64 * DET_MAX_CHUNK - 1) / (64 * DET_MAX_CHUNK);
-    const int chunk = ((Lc + 64 * R - 1) / (64 * R)) | 1;
+    const int c0 = ((Lc + 64 * R - 1) / (64 * R)) | 1, c1 = c0, B1 = 64 * c0;
+#endif
     // Items go out in runs of FRAME_ITEM_RUN per wave: wave gw starts with run gw, the runs past the first
     // gridDim.x * SYNC_WAVES come from a per-launch atomic counter, so waves that run fast take more runs.
     // Lane 0 fetches the next run at the first item of the current one (its wait is paid once per run).
@@ -456,57 +531,18 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
         const float *r = rbase + off;                       // r[n] = Re capture sample n
         // Im capture sample n = imt[im0 + n] reduced mod the period (a.im_period: nfilt, or 2^30 for ext)
         const int im0 = ext ? 0 : im_mod(a, rx_start);
+        // lazy capture + detection (FRAME_LAZY): not for external captures, dumps or the word-length report,
+        // which read the whole capture
+        const bool lazy = FRAME_LAZY && !a.no_lazy && !ext && R == 2 && !a.word_stats && !a.dbg_corr &&
+                          !(a.dbg_frame && first_item);
+        int b1s = 0;                                         // last Philox block generated
         if (ext) {
             for (int n = lane; n < L; n += 64) rbase[off + n] = a.ext[n].x;
         } else {
+            // lazy: the blocks of capture samples [0, B1 + 47) first (round 0 reads them), the rest on demand
             const int b0 = rx_start >> 2, b1 = (rx_start + L - 1) >> 2;
-            const PhiloxHead hd = philox_head(t_lo, t_hi, STREAM_NOISE | qs, a.k1);
-            const float Ksig = noise_k(sigma);
-#ifndef FRAME_CAP_SKEYS
-            // round keys in VGPRs: each round's two v_bitop3_b32 issue at the fast rate (an SGPR operand makes
-            // them slow-class); 20 VGPRs for the capture loop only
-            PhiloxKeysV vk;
-            vk.init(a.k0, a.k1);
-#endif
-            // Gaussian k of the trial's stream goes to waveform sample k (as if Transmission_Over_Air had drawn
-            // the whole waveform); only the captured samples are ever evaluated.  The waveform is FR_REPS
-            // copies of one filtered frame (OFDM.c:607-612): sample k is sample k mod nfilt of the first copy
-            // (7.8 KB, L1-resident).  bm = the block's index within the copy.
-            const uint32_t pb = (uint32_t)(a.wave_len / (4 * FR_REPS)), nb_wave = (uint32_t)(a.wave_len / 4);
-            uint32_t bm = (uint32_t)(b0 + lane) % pb;
-#ifndef FRAME_CAP_U
-#define FRAME_CAP_U 6   // Philox blocks per lane per pass: 12 of a reference capture in 2 passes (A/B: +0.8 % over 3)
-#endif
-            for (int bb = b0 + lane; bb <= b1; bb += FRAME_CAP_U * 64) {
-                float4 v[FRAME_CAP_U];
-#pragma unroll
-                for (int u = 0; u < FRAME_CAP_U; ++u) {
-                    const int b = bb + 64 * u;
-                    const float4 *s4 = reinterpret_cast<const float4 *>(a.wave + 4 * bm);
-                    const bool in = b <= b1 && (uint32_t)b < nb_wave;
-                    const float4 lo = in ? s4[0] : make_float4(0.f, 0.f, 0.f, 0.f);
-                    const float4 hi = in ? s4[1] : make_float4(0.f, 0.f, 0.f, 0.f);
-                    v[u] = make_float4(lo.x, lo.z, hi.x, hi.z);
-                    bm = bm + 64 >= pb ? bm + 64 - pb : bm + 64;           // (bm + 64) mod pb (pb > 64)
-                }
-#pragma unroll
-                for (int u = 0; u < FRAME_CAP_U; ++u) {
-                    const int b = bb + 64 * u;
-                    if (b > b1) break;
-                    float4 w = v[u];
-                    if (a.noise == OFDM_NOISE_REAL) {   // real-only (D7): sigma z = sqrt(K log2 u1) (cos | sin)
-#ifndef FRAME_CAP_SKEYS
-                        const Noise4 nz = noise4_of(philox10_c2(hd, (uint32_t)b, vk), Ksig);
-#else
-                        const Noise4 nz = noise4_of(philox10_c2(hd, (uint32_t)b, a.k0, a.k1), Ksig);
-#endif
-                        w.x = fmaf(nz.r0, nz.c0, w.x); w.y = fmaf(nz.r0, nz.s0, w.y);
-                        w.z = fmaf(nz.r1, nz.c1, w.z); w.w = fmaf(nz.r1, nz.s1, w.w);
-                    }
-                    // samples of the block outside [0, L) land in the region's slack, never read as capture
-                    *reinterpret_cast<float4 *>(rbase + 4 * (b - b0)) = w;
-                }
-            }
+            b1s = lazy ? min((rx_start + B1 + 46) >> 2, b1) : b1;
+            capture_blocks(a, rbase, b0, b0, b1s, lane, t_lo, t_hi, qs, sigma);
         }
         wave_lds_sync();
         FR_STAMP(0);                                           // capture + noise
@@ -545,12 +581,14 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
         // positions per batch.  M > 0.75 (OFDM.c:687, 695) is decided as the sign of
         // t = 0.75 den - num (fma: exact before its one rounding): t < 0 <=> crossing, which keeps the
         // division's outcomes 0/0 -> false (t = +0) and x/0 -> true (t = -num).  Lane l of round rho owns
-        // positions [(64 rho + l) chunk, +chunk); crossing n at bit n - n0 of the round's mask. ----
+        // positions [base + l chunk, +chunk) (round 0: base 0, chunk c0; round 1: B1, c1); crossing n at bit n - n0
+        // of the round's mask. ----
         unsigned long long cm[2] = {0ull, 0ull};
         int first[2] = {-1, -1}, last[2] = {-1, -1};
-        static_for<0, 2>([&](auto rc) {
+        auto detect = [&](auto rc) {
             constexpr int rho = decltype(rc)::value;
-            const int n0 = (64 * rho + lx) * chunk, n1 = min(n0 + chunk, Lc);
+            const int chunk = rho ? c1 : c0;
+            const int n0 = (rho ? B1 : 0) + lx * chunk, n1 = min(n0 + chunk, Lc);
             unsigned long long cmask = 0ull;
             if (rho < R && n0 < n1) {
                 const float *ti_ = imt + im_mod(a, im0 + n0);   // Im of sample n0 + k at ti_[k] (k < IMT_EXT)
@@ -615,7 +653,47 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
             cm[rho] = cmask;
             first[rho] = cmask ? n0 + __builtin_ctzll(cmask) : -1;
             last[rho] = cmask ? n0 + 63 - __builtin_clzll(cmask) : -1;
-        });
+        };
+        // the crossing bit of position pos (< Lc) from the lane that owns it (ds_bpermute)
+        auto crossing = [&](int pos) {
+            const int rp = pos >= B1, chp = rp ? c1 : c0, rel = pos - (rp ? B1 : 0);
+            const int v = rel / chp, owner = v & 63, bit = rel - v * chp;
+            unsigned long long w = 0ull;
+            static_for<0, 2>([&](auto r2c) {
+                constexpr int r2 = decltype(r2c)::value;
+                if (r2 < R) {
+                    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)cm[r2], owner, 64);
+                    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(cm[r2] >> 32), owner, 64);
+                    if (rp == r2) w = ((unsigned long long)hi << 32) | lo;
+                }
+            });
+            return ((w >> bit) & 1ull) != 0ull;
+        };
+        detect(std::integral_constant<int, 0>{});
+        // Lazy: round 0 decides Packet_Selection when its least valid front f (M[f + 230] > 0.75 with f + 230 < B1)
+        // has a later front in round 0 -- every earlier front is > 300 before f, so its own check lies in round 0
+        // and failed, and neither the fronts nor their checks before f depend on round 1 -- and the matched
+        // filter's samples [p - 20, p + 2 (nfr - 1) + 10] lie in the generated part.
+        bool decided = false;
+        int cand0 = 0x7fffffff;
+        if (lazy) {
+            const int pm = wave_prefix_max(last[0]);
+            const int prev = max(wave_shr1(pm), -1);
+            const int front = (first[0] >= 0 && first[0] - prev > 300) ? first[0] : -1;
+            const int pos = front + 230;
+            const bool valid = crossing(pos < B1 ? pos : 0) && front >= 0 && pos < B1;
+            const int vmin0 = wave_min_i(valid ? front : 0x7fffffff), fmax0 = wave_max_i(front);
+            const int gen = 4 * (b1s + 1) - rx_start;            // capture samples generated: [0, gen)
+            decided = vmin0 < fmax0 && vmin0 + 11 + 2 * (nfr - 1) + 10 < gen;
+            cand0 = vmin0;
+        }
+        if (R == 2 && !decided) {
+            if (lazy) {                                          // the rest of the capture, then round 1
+                capture_blocks(a, rbase, rx_start >> 2, b1s + 1, (rx_start + L - 1) >> 2, lane, t_lo, t_hi, qs, sigma);
+                wave_lds_sync();
+            }
+            detect(std::integral_constant<int, 1>{});
+        }
         if (a.dbg_corr && first_item) {             // Corr_Out for ofdm_receiver's parity dump
             for (int n = lx; n < Lc; n += 64) {
                 float sx = 0.f, sy = 0.f, pw = 0.f;
@@ -636,34 +714,26 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
         // crossing can be one, and its predecessor is the last crossing of the earlier chunks: an exclusive
         // prefix max over (round, lane).  The first front x with a later front and M[front+230] > 0.75 gives
         // packet_idx = front + len_RRC_rx + 1; otherwise 0 (OFDM.c:752-761). ----
-        int vmin = 0x7fffffff, fmax_ = -1, carry = -1;
-        static_for<0, 2>([&](auto rc) {
-            constexpr int rho = decltype(rc)::value;
-            if (rho < R) {
-                const int pm = max(wave_prefix_max(last[rho]), carry);
-                const int prev = max(wave_shr1(pm), carry);
-                const int front = (first[rho] >= 0 && first[rho] - prev > 300) ? first[rho] : -1;
-                carry = __builtin_amdgcn_readlane(pm, 63);
-                // the crossing bit of position front + 230 from the lane that owns it (ds_bpermute)
-                const int pos = front + 230;
-                const int v = pos / chunk, owner = v & 63, bit = pos - v * chunk;
-                unsigned long long w = 0ull;
-                static_for<0, 2>([&](auto r2c) {
-                    constexpr int r2 = decltype(r2c)::value;
-                    if (r2 < R) {
-                        const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)cm[r2], owner, 64);
-                        const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(cm[r2] >> 32), owner, 64);
-                        if ((v >> 6) == r2) w = ((unsigned long long)hi << 32) | lo;
-                    }
-                });
-                const bool valid = front >= 0 && pos < Lc && ((w >> bit) & 1ull);
-                vmin = min(vmin, valid ? front : 0x7fffffff);
-                fmax_ = max(fmax_, front);
-            }
-        });
-        // the first valid front that has a later front: the least valid front, unless it is the last one
-        const int cmin = wave_min_i(vmin), cmax = wave_max_i(fmax_);
-        const int cand = cmin < cmax ? cmin : 0x7fffffff;
+        int cand = cand0;
+        if (!decided) {
+            int vmin = 0x7fffffff, fmax_ = -1, carry = -1;
+            static_for<0, 2>([&](auto rc) {
+                constexpr int rho = decltype(rc)::value;
+                if (rho < R) {
+                    const int pm = max(wave_prefix_max(last[rho]), carry);
+                    const int prev = max(wave_shr1(pm), carry);
+                    const int front = (first[rho] >= 0 && first[rho] - prev > 300) ? first[rho] : -1;
+                    carry = __builtin_amdgcn_readlane(pm, 63);
+                    const int pos = front + 230;
+                    const bool valid = crossing(pos < Lc ? pos : 0) && front >= 0 && pos < Lc;
+                    vmin = min(vmin, valid ? front : 0x7fffffff);
+                    fmax_ = max(fmax_, front);
+                }
+            });
+            // the first valid front that has a later front: the least valid front, unless it is the last one
+            const int cmin = wave_min_i(vmin), cmax = wave_max_i(fmax_);
+            cand = cmin < cmax ? cmin : 0x7fffffff;
+        }
         const bool sync_fail = cand == 0x7fffffff;
         const int p = sync_fail ? 0 : cand + 10 + 1;           // len_RRC_rx + 1 (OFDM.c:758)
         FR_STAMP(2);                                           // packet selection
@@ -1061,6 +1131,8 @@ static void fill_frame_args(FrameArgs &a, Ctx *c, const ofdm_rx_opts *o, int noi
     a.n_data = payload_table(payload, c->message, a.table);
     for (int d = 0; d < a.n_data; ++d) demap_words(a.table + 3 * d, a.dtable + 4 * d);
     a.word_stats = o->word_stats ? 1 : 0;
+    // the lazy capture's equivalence test runs the same sweep with it switched off (tests/test_gpu_frame.py)
+    a.no_lazy = getenv("OFDM_FRAME_NO_LAZY") != nullptr;
     rrc_taps(a.taps);
 }
 

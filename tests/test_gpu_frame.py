@@ -106,6 +106,32 @@ def test_frame_sweep_vs_oracle(engine, oracle, pkg):
     assert np.all(np.abs(g[:, 5] - o[:, 5]) <= np.sum(gp != op, axis=1))
 
 
+def test_lazy_capture_equals_full_evaluation(engine, pkg, monkeypatch):
+    """The sync kernel generates the rest of a capture and runs its second detection round only when the
+    first round (positions [0, 1984) of the reference capture) does not decide Packet_Selection
+    (OFDM.c:685-771) or the matched filter would read past the generated samples.  Every counter and every
+    packet_idx must equal the full evaluation's (OFDM_FRAME_NO_LAZY) on the same streams, over the bench's
+    SNR grid and for an 8-symbol message (two long detection rounds)."""
+    snrs = np.arange(0.0, 31.0, 2.0)
+    cfg = pkg.make_cfg(payload="message")
+    lazy, lp = engine.frame_sweep(cfg, snrs, 3000, want_packet_idx=True)
+    monkeypatch.setenv("OFDM_FRAME_NO_LAZY", "1")
+    full, fp = engine.frame_sweep(cfg, snrs, 3000, want_packet_idx=True)
+    assert np.array_equal(lp, fp)
+    assert np.array_equal(lazy, full)
+    assert np.mean(lp[8:] > 0) > 0.99                         # >= 16 dB: nearly every trial synchronises
+    monkeypatch.delenv("OFDM_FRAME_NO_LAZY")
+    msg = (b"lazy capture, eight data symbols. " * 3)[:96]
+    with pkg.Engine(0) as e8:
+        assert e8.set_message(msg) == 8
+        cfg8 = pkg.make_cfg(payload="message")
+        lazy8, lp8 = e8.frame_sweep(cfg8, snrs[::3], 500, want_packet_idx=True)
+        monkeypatch.setenv("OFDM_FRAME_NO_LAZY", "1")
+        full8, fp8 = e8.frame_sweep(cfg8, snrs[::3], 500, want_packet_idx=True)
+    assert np.array_equal(lp8, fp8)
+    assert np.array_equal(lazy8, full8)
+
+
 def _drop_trials(sweep, snrs, trials, n_counters=16):
     """counters of the given trials (one call each, same SNR grid, so the same streams)"""
     acc = np.zeros((len(snrs), n_counters), np.int64)
