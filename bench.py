@@ -83,6 +83,13 @@ def issue_cap(pmc: dict, frac: float) -> dict:
     m = pmc.get("issue_model")
     if not m:
         return {}
+    if m.get("method") == "dynamic":     # tools/mix_cap.py: the measured class mix, ambiguous classes bounded
+        lo, hi = m["cap_frac_range"]
+        return {"issue_model_cap_frac": lo, "issue_model_cap_frac_range": [lo, hi],
+                "frac_of_issue_model_cap": frac / lo, "frac_of_issue_model_cap_range": [frac / hi, frac / lo],
+                "issue_model_note": "cap = 2 x VALU / SIMD cycles of the dynamic class mix (PMC class counters) at "
+                                    "%d waves/SIMD, unclassified instructions priced slow (cap) or fast (upper end)"
+                                    % m["waves_per_simd"]}
     return {"issue_model_cap_frac": m["cap_frac"], "frac_of_issue_model_cap": frac / m["cap_frac"],
             "issue_model_note": "cap = 2 x loop VALU / class-priced SIMD cycles at %d waves/SIMD (modelled)"
                                 % m["waves_per_simd"]}

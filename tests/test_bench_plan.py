@@ -125,6 +125,33 @@ def test_roofline_needs_pmc_of_the_loaded_build(pkg):
     assert r["frac"] is not None and "issue_model_cap_frac" not in r
 
 
+def test_dynamic_mix_cap(tmp_path):
+    """tools/mix_cap.py prices the measured class counters (ambiguous classes once slow, once fast) and
+    bench.py reports the run's fraction of both ends of that range."""
+    sys.path.insert(0, str(ROOT / "tools"))
+    import mix_cap
+    from isa_mix import COST
+    c = {"SQ_INSTS_VALU": 100.0, "SQ_INSTS_VALU_FMA_F32": 50.0, "SQ_INSTS_VALU_TRANS_F32": 10.0,
+         "SQ_INSTS_VALU_INT64": 10.0}
+    lo, hi, shares = mix_cap.price(c, 3)
+    k = COST[3]
+    assert lo == pytest.approx(200 / (50 * k["fast"] + 10 * k["trans"] + 40 * k["slow"]))
+    assert hi == pytest.approx(200 / (80 * k["fast"] + 10 * k["trans"] + 10 * k["slow"]))
+    assert shares["ambiguous"] == pytest.approx(0.3) and lo < hi
+    rows = [{"Kernel_Name": "ofdm::frame_sync_kernel(ofdm::FrameArgs)", "Counter_Name": n, "Counter_Value": str(v)}
+            for n, v in c.items()]
+    d = tmp_path / "pass"
+    d.mkdir()
+    with open(d / "run_counter_collection.csv", "w") as f:
+        f.write("Kernel_Name,Counter_Name,Counter_Value\n")
+        f.writelines(f"\"{r['Kernel_Name']}\",{r['Counter_Name']},{r['Counter_Value']}\n" for r in rows)
+    assert mix_cap.counters([d, d], mix_cap.SETS["frame"])["SQ_INSTS_VALU"] == 100.0   # counted once
+    b = _bench()
+    cap = b.issue_cap({"issue_model": {"method": "dynamic", "cap_frac": lo, "cap_frac_range": [lo, hi],
+                                       "waves_per_simd": 3}}, 0.5)
+    assert cap["frac_of_issue_model_cap_range"] == pytest.approx([0.5 / hi, 0.5 / lo])
+
+
 def test_kernel_build_id_tracks_code_bytes(pkg, tmp_path):
     """The id is a hash of the kernel's machine code: flipping one byte of it in a copy of the library
     changes the id of that workload and no other's."""
