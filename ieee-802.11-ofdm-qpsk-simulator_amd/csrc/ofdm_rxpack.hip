@@ -433,10 +433,20 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
                     uint32_t tg = 48u + 2 * i;
                     opaque(tg);
                     // blocks b = 2i, 2i+1 (z[4i..4i+3]) and b + 8 (z[4i+16..4i+19])
+#ifdef OFDM_PACK_VK4       // A/B: the four blocks' rounds together, round keys in 2 VGPRs advanced per round
+                    uint4 o4[4];
+                    const uint32_t c2s[4] = {tg, tg + 8, tg + 1, tg + 9};
+                    philox10_c2_vk<4>(hd, c2s, a.k0, a.k1, o4);
+#endif
                     static_for<0, 2>([&](auto hc) {
                         constexpr int h = decltype(hc)::value;
+#ifdef OFDM_PACK_VK4
+                        const Noise4 lo = noise4_of(o4[2 * h], KE);
+                        const Noise4 hi = noise4_of(o4[2 * h + 1], KE);
+#else
                         const Noise4 lo = pack_noise(hd, tg + h, PKEYS, KE);
                         const Noise4 hi = pack_noise(hd, tg + 8 + h, PKEYS, KE);
+#endif
                         constexpr int m = 4 * i + 2 * h;
                         z[m] = make_float2(lo.r0 * lo.c0, -(lo.r0 * lo.s0));
                         z[m + 1] = make_float2(lo.r1 * lo.c1, -(lo.r1 * lo.s1));
@@ -581,10 +591,22 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
                 constexpr int g = decltype(gc)::value;
                 uint32_t tg = 84u + g;
                 opaque(tg);
+#ifdef OFDM_PACK_VK4
+                uint4 o4[4];
+#endif
                 static_for<0, 4>([&](auto Qc) {
                     constexpr int Q = decltype(Qc)::value;
+#ifdef OFDM_PACK_VK4
+                    if constexpr ((Q & 1) == 0) {
+                        const uint32_t c2s[4] = {tg + 4 * Q, tg + 20 + 4 * Q, tg + 4 * Q + 4, tg + 24 + 4 * Q};
+                        philox10_c2_vk<4>(hd, c2s, a.k0, a.k1, o4);
+                    }
+                    const Noise4 n0 = noise4_of(o4[2 * (Q & 1)], K);
+                    const Noise4 n1 = noise4_of(o4[2 * (Q & 1) + 1], K);
+#else
                     const Noise4 n0 = pack_noise(hd, tg + 4 * Q, PKEYS, K);
                     const Noise4 n1 = pack_noise(hd, tg + 20 + 4 * Q, PKEYS, K);
+#endif
                     const float d0[4] = {n0.r0 * n0.c0, n0.r0 * n0.s0, n0.r1 * n0.c1, n0.r1 * n0.s1};
                     const float d1[4] = {n1.r0 * n1.c0, n1.r0 * n1.s0, n1.r1 * n1.c1, n1.r1 * n1.s1};
                     static_for<0, 4>([&](auto ic) {

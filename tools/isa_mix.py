@@ -5,7 +5,8 @@ usage: python tools/isa_mix.py <asm.s> <mangled kernel name> [--loop N]
 Classes follow the measured issue costs (profiles/r01/ubench/ubench_bank_forms.txt, SIMD cycles per
 wave64 instruction at 2 / 4 waves per SIMD):
   fast   v_add/sub/mul/fma/fmac/fmamk/fmaak_f32, v_add/sub_u32, v_and/or/xor_b32, v_bitop3_b32 with
-         VGPR / inline-constant operands (and VOP2 literals)                     2.35 / 1.97
+         VGPR / inline-constant operands (and VOP2 literals); v_bitop3_b32 also with an SGPR operand
+         (measured in the receivers, profiles/r03/ab_o)                          2.35 / 1.97
   slow   any SGPR operand; shifts, alignbit, cvt, max/min, bfe, perm, mul_lo/hi, DPP, cndmask_e64,
          v_mad_u64_u32 (3.22 at 4 waves)                                         4.30 / 3.15
   trans  v_log/sin/cos/sqrt/rcp/exp_f32                                          8.23 / 6.12
@@ -23,6 +24,11 @@ ROOT = Path(__file__).resolve().parents[1]
 FAST_OPS = re.compile(r"^v_(add|sub|subrev|mul|fma|fmac|fmamk|fmaak)_f32|^v_(add|sub|subrev)_u32|^v_(and|or|xor)_b32"
                       r"|^v_bitop3_b32|^v_mov_b32|^v_add_co_u32|^v_sub_co_u32")
 TRANS = re.compile(r"^v_(log|sin|cos|sqrt|rcp|exp|rsq)_f32")
+# v_bitop3_b32 with an SGPR operand (the Philox round keys) issues at the fast rate inside the receivers: moving
+# the keys to VGPRs measured +0.3 % (20 VGPRs of keys) and -4 % (2 VGPRs advanced per round, +240 v_add per
+# iteration) on c3, where the SGPR-slow pricing predicted +5 % (profiles/r03/ab_o/), unlike the isolated
+# microbenchmark form of profiles/r01/ubench
+SGPR_FAST = re.compile(r"^v_bitop3_b32")
 COST = {2: {"fast": 2.35, "slow": 4.30, "trans": 8.23, "cnd": 16.2},
         4: {"fast": 1.97, "slow": 3.15, "trans": 6.12, "cnd": 12.5}}
 COST[3] = {k: 0.5 * (COST[2][k] + COST[4][k]) for k in COST[2]}     # interpolated (not measured)
@@ -40,7 +46,7 @@ def classify(op, args):
     sgpr = re.search(r"(?<![\w])s\d+|s\[\d+", args) is not None
     if "dpp" in args or "quad_perm" in args or "row_" in args:
         return "slow"
-    if FAST_OPS.match(op) and not sgpr:
+    if FAST_OPS.match(op) and (not sgpr or SGPR_FAST.match(op)):
         return "fast"
     return "slow"
 
