@@ -412,7 +412,7 @@ __device__ __forceinline__ void capture_blocks(const A &a, float *rbase, int b0,
     const uint32_t pb = (uint32_t)(a.wave_len / (4 * FR_REPS)), nb_wave = (uint32_t)(a.wave_len / 4);
     uint32_t bm = (uint32_t)(bs + lane) % pb;
 #ifndef FRAME_CAP_U
-#define FRAME_CAP_U 6   // Philox blocks per lane per pass: 12 of a reference capture in 2 passes (A/B: +0.8 % over 3)
+#define FRAME_CAP_U 4   // Philox blocks per lane per pass: the lazy capture's 8 + 4 blocks in passes of 4 (A/B: +1.3 % over 6, = 8)
 #endif
     for (int bb = bs + lane; bb <= be; bb += FRAME_CAP_U * 64) {
         float4 v[FRAME_CAP_U];
