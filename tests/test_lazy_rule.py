@@ -1,0 +1,59 @@
+"""The frame sync kernel's lazy capture rule (ofdm_frame.hip, FRAME_LAZY) against the
+reference's own Packet_Selection (src/OFDM.c:685-771, compiled in oracle/_ref) on random captures of the
+reference waveform: whenever the first detection round [0, 64 x 31) decides the selection by the kernel's
+rule, the reference's packet_idx over the WHOLE capture is that decision.  (The GPU test
+test_lazy_capture_equals_full_evaluation checks the kernel's lazy and full paths against each other.)"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+B1 = 64 * 31                 # round 0 of the reference capture (FRAME_LAZY_C0 = 31)
+NFR = 320 + 80 * 2           # fr_len of the 2-symbol reference message
+LEN_RRC_RX = 10
+
+
+def corr_out(cap):
+    """Packet_Detection (OFDM.c:659-683): M[i] = |sum r[i+k] r[i+k+16]|^2 / (sum |r[i+k+16]|^2)^2, k < 32"""
+    lc = len(cap) - 47
+    prod = cap[:-16] * cap[16:]
+    pw = np.abs(cap[16:]) ** 2
+    cs = np.concatenate([[0], np.cumsum(prod)])
+    cp = np.concatenate([[0], np.cumsum(pw)])
+    n = np.arange(lc)
+    return (np.abs(cs[n + 32] - cs[n]) ** 2 / (cp[n + 32] - cp[n]) ** 2).astype(np.float32)
+
+
+def lazy_decision(m, rx_start):
+    """the kernel's rule: (decided, packet_idx) from round 0 alone"""
+    idx = np.nonzero(m[:B1] > 0.75)[0]
+    prev = np.concatenate([[-1], idx[:-1]])
+    fronts = idx[(idx - prev) > 300]
+    valid = [f for f in fronts if f + 230 < B1 and m[f + 230] > 0.75]
+    if not valid or valid[0] >= fronts.max():
+        return False, None
+    f = valid[0]
+    gen = 4 * (((rx_start + B1 + 46) >> 2) + 1) - rx_start          # capture samples generated before round 0
+    if f + LEN_RRC_RX + 1 + 2 * (NFR - 1) + 10 >= gen:
+        return False, None
+    return True, int(f) + LEN_RRC_RX + 1
+
+
+@pytest.mark.parametrize("snr_db", [0.0, 6.0, 9.0, 12.0, 16.0, 30.0])
+def test_round0_decision_is_the_references(reflib, snr_db):
+    wave = reflib.waveform().astype(np.complex128)
+    L = int(0.307 * len(wave))
+    rng = np.random.default_rng(int(snr_db * 10) + 1)
+    sigma = np.sqrt(np.mean(np.abs(wave) ** 2) / 10 ** (snr_db / 10))
+    decided = 0
+    for _ in range(400):
+        s = int(rng.integers(0, len(wave) - L))
+        cap = wave[s:s + L] + sigma * rng.standard_normal(L)        # real-only AWGN (D7)
+        m = corr_out(cap)
+        ok, p = lazy_decision(m, s)
+        if ok:
+            decided += 1
+            ref = reflib.lib.ref_packet_selection(m.ctypes.data_as(C.c_void_p), len(m))
+            assert ref == p, (snr_db, s)
+    if snr_db >= 12:
+        assert decided > 0.6 * 400                                  # the rule does skip work where sync works
