@@ -388,6 +388,9 @@ __device__ __forceinline__ void lds_readn(const float *p, int s, float (&x)[N]) 
 #ifndef FRAME_LAZY
 #define FRAME_LAZY 1        // lazy capture + detection (see frame_sync_kernel; A/B: +5.3 %, profiles/r03/ab_n/)
 #endif
+#ifndef FRAME_R1_SPREAD
+#define FRAME_R1_SPREAD 1   // round 1 in one 16-position batch where spread chunks allow (A/B option)
+#endif
 #ifndef FRAME_LAZY_C0
 #define FRAME_LAZY_C0 31    // round-0 positions per lane when lazy (two 16-position batches)
 #endif
@@ -484,12 +487,21 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
     const int c0 = Lc > 64 * FRAME_LAZY_C0 ? FRAME_LAZY_C0 : (((Lc + 63) / 64) | 1);
     const int B1 = 64 * c0;
     const int R = Lc > B1 ? 2 : 1;
-    const int c1 = R == 2 ? (((Lc - B1 + 63) / 64) | 1) : c0;
+    // round 1: a uniform odd chunk, or -- when that saves a 16-position batch (the reference capture: 977
+    // positions = 64 x 15 + 17, one batch instead of two of chunk 17) -- c1 positions per lane plus one more on
+    // x1 lanes spread evenly (lane l starts at B1 + l c1 + floor(l x1 / 64): at most 2-way LDS bank conflicts)
+    int c1 = R == 2 ? (((Lc - B1 + 63) / 64) | 1) : c0, x1 = 0;
+    if (R == 2) {
+        const int c1b = (Lc - B1) / 64, r1 = (Lc - B1) - 64 * c1b;
+        if (FRAME_R1_SPREAD && (c1b + (r1 > 0) + DET_B - 1) / DET_B < (c1 + DET_B - 1) / DET_B) { c1 = c1b; x1 = r1; }
+    }
 #else
     // one round for the reference capture (chunk 47)
     const int R = (Lc + 64 * DET_MAX_CHUNK - 1) / (64 * DET_MAX_CHUNK);
-    const int c0 = ((Lc + 64 * R - 1) / (64 * R)) | 1, c1 = c0, B1 = 64 * c0;
+    const int c0 = ((Lc + 64 * R - 1) / (64 * R)) | 1, c1 = c0, B1 = 64 * c0, x1 = 0;
 #endif
+    // first position of lane l's round-1 chunk, relative to B1
+    auto r1_start = [c1, x1](int l) { return l * c1 + ((l * x1) >> 6); };
     // Items go out in runs of FRAME_ITEM_RUN per wave: wave gw starts with run gw, the runs past the first
     // gridDim.x * SYNC_WAVES come from a per-launch atomic counter, so waves that run fast take more runs.
     // Lane 0 fetches the next run at the first item of the current one (its wait is paid once per run).
@@ -587,15 +599,15 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
         int first[2] = {-1, -1}, last[2] = {-1, -1};
         auto detect = [&](auto rc) {
             constexpr int rho = decltype(rc)::value;
-            const int chunk = rho ? c1 : c0;
-            const int n0 = (rho ? B1 : 0) + lx * chunk, n1 = min(n0 + chunk, Lc);
+            const int chunk = rho ? r1_start(lx + 1) - r1_start(lx) : c0;
+            const int n0 = rho ? B1 + r1_start(lx) : lx * c0, n1 = min(n0 + chunk, Lc);
             unsigned long long cmask = 0ull;
             if (rho < R && n0 < n1) {
                 const float *ti_ = imt + im_mod(a, im0 + n0);   // Im of sample n0 + k at ti_[k] (k < IMT_EXT)
                 const float *tr_ = r + n0;
                 float sx = 0.f, sy = 0.f, pw = 0.f;
                 uint32_t mlo = 0u, mhi = 0u;
-                const int nbat = (chunk + DET_B - 1) / DET_B;
+                const int nbat = ((rho ? c1 + (x1 > 0) : c0) + DET_B - 1) / DET_B;   // uniform over the lanes
                 // Samples in register blocks of DET_B: position n's window terms read samples n (leaving), n + 16,
                 // n + 32 and n + 48 (entering), i.e. blocks b, b + 1, b + 2, b + 3 of batch b, so every sample is
                 // loaded from LDS once (ds_read2_b32) instead of four times (A/B: +2.3 % frame mode, 167 VGPRs).
@@ -656,8 +668,16 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
         };
         // the crossing bit of position pos (< Lc) from the lane that owns it (ds_bpermute)
         auto crossing = [&](int pos) {
-            const int rp = pos >= B1, chp = rp ? c1 : c0, rel = pos - (rp ? B1 : 0);
-            const int v = rel / chp, owner = v & 63, bit = rel - v * chp;
+            const int rp = pos >= B1, rel = pos - (rp ? B1 : 0);
+            int v;
+            if (!rp) {
+                v = rel / c0;
+            } else {                                             // the lane whose round-1 chunk holds rel
+                v = (rel * 64) / (64 * c1 + x1);
+                if (r1_start(v + 1) <= rel) ++v;
+                else if (r1_start(v) > rel) --v;
+            }
+            const int owner = v & 63, bit = rel - (rp ? r1_start(v) : v * c0);
             unsigned long long w = 0ull;
             static_for<0, 2>([&](auto r2c) {
                 constexpr int r2 = decltype(r2c)::value;
