@@ -61,7 +61,9 @@ WORKLOADS = {
            "1e9 symbol-SNR evaluations in total (6.25e7 symbols/point x 16) over the ranks",
            dict(est="ls", noise="real", channel="rayleigh4", conv="c", payload="random"),
            62_500_000, "strong"),
-    "frame": ("frame mode: OFDM.c Transmission_Over_Air + Receiver trials (sync, CFO, LS), reference message",
+    "frame": ("frame mode: OFDM.c Transmission_Over_Air + Receiver trials (sync, CFO, LS), reference message; the "
+              "capture's tail is generated only when the first detection round does not decide Packet_Selection "
+              "(results bit-identical to full evaluation, OFDM_FRAME_NO_LAZY)",
               dict(payload="message", noise="real", conv="c"), 1_000_000, "weak"),
 }
 
