@@ -132,6 +132,20 @@ def test_lazy_capture_equals_full_evaluation(engine, pkg, monkeypatch):
     assert np.array_equal(lazy8, full8)
 
 
+def test_frame_sweep_two_chunks_equal_their_halves(engine, pkg):
+    """A sweep of more than 2^22 (trial, SNR) items runs as several sync -> symbol launch pairs through the
+    hand-off buffer: its counters and packet_idx equal those of two sweeps of half the trials each (one
+    chunk each)."""
+    cfg = pkg.make_cfg(payload="message")
+    snrs = np.arange(0.0, 31.0, 2.0)
+    n = 300_000                                   # 4.8M items: two chunks
+    whole, wp = engine.frame_sweep(cfg, snrs, n, want_packet_idx=True)
+    a, ap = engine.frame_sweep(cfg, snrs, n // 2, want_packet_idx=True)
+    b, bp = engine.frame_sweep(cfg, snrs, n // 2, first_trial=n // 2, want_packet_idx=True)
+    assert np.array_equal(wp, np.concatenate([ap, bp], axis=1))
+    assert np.array_equal(whole, a + b)
+
+
 def _drop_trials(sweep, snrs, trials, n_counters=16):
     """counters of the given trials (one call each, same SNR grid, so the same streams)"""
     acc = np.zeros((len(snrs), n_counters), np.int64)
