@@ -240,6 +240,7 @@ class RefLib:
         L.ref_toa.argtypes = [C.c_void_p, C.c_void_p, C.c_float, C.c_int]
         L.ref_trial.argtypes = [C.c_float, C.c_void_p]
         L.ref_seed.argtypes = [C.c_uint64]
+        L.ref_seed_bits.argtypes = [C.c_uint64]
         L.ref_packet_selection.restype = C.c_int
         L.ref_time_symbol_chain.restype = C.c_double
         L.ref_time_symbol_chain.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
@@ -335,3 +336,14 @@ class RefLib:
         t = self.lib.ref_time_symbol_chain(_p(snr), len(snr), int(n_frames), int(rayleigh) | 2 * int(ideal),
                                             _p(acc))
         return t, acc
+
+    def symbol_chain_stats(self, snr_db: float, n_frames: int, seed: int):
+        """The same chain at one SNR point for a golden fixture (gen_golden.py --only chain): noise and payload
+        streams seeded by `seed`; returns [bit errors, bits, sum|z-d|^2, sum of per-frame bit errors^2,
+        frames with an error]."""
+        snr = np.ascontiguousarray([snr_db], np.float32)
+        acc = np.zeros(5, np.float64)
+        self.lib.ref_seed(C.c_uint64(seed))
+        self.lib.ref_seed_bits(C.c_uint64(0x9E3779B97F4A7C15 ^ (seed * 0x2545F4914F6CDD1D % (1 << 64))))
+        self.lib.ref_time_symbol_chain(_p(snr), 1, int(n_frames), 4, _p(acc))
+        return acc

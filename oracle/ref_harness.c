@@ -387,6 +387,9 @@ void ref_gaussian_noise(int n, float *out)
  * flags bit 1 (config c2, ideal CSI): the known channel instead of the LTF estimate -- H is taken once
  * from Channel_Estimation of the noiseless frame (AWGN: the exact channel of the fft(ifft()) pair) and
  * the per-SNR Channel_Estimation is skipped, as the GPU's ideal-CSI receiver skips it.
+ * flags bit 2 (fixture statistics, tests/golden/gen_golden.py --only chain): acc is double[5] and also gets
+ * acc[3] += sum over (frame, SNR) of (bit errors of the frame)^2, acc[4] += frames with a bit error, the
+ * frame-clustered variance of the BER estimate.
  * acc3 += {bit errors, bits, sum |z - d|^2}.  Returns wall seconds.
  */
 static unsigned long long g_bits_state = 0x9E3779B97F4A7C15ULL;
@@ -395,6 +398,8 @@ static unsigned int bits_next(void)
     g_bits_state ^= g_bits_state << 13; g_bits_state ^= g_bits_state >> 7; g_bits_state ^= g_bits_state << 17;
     return (unsigned int)(g_bits_state >> 11);
 }
+/* payload bits of independent fixture jobs: any non-zero state */
+void ref_seed_bits(unsigned long long s) { g_bits_state = s ? s : 0x9E3779B97F4A7C15ULL; }
 
 double ref_time_symbol_chain(const float *snr_db, int n_snr, int n_frames, int flags, double *acc3)
 {
@@ -410,7 +415,7 @@ double ref_time_symbol_chain(const float *snr_db, int n_snr, int n_frames, int f
     float complex **rx_time = Allocate_Array_2D(D, 64), **rx_freq = Allocate_Array_2D(D, 64);
     float complex **no_pilot = Allocate_Array_2D(D, 48), **final = Allocate_Array_2D(D, 48);
     float complex **demod = Allocate_Array_2D(D, 96);
-    double be = 0, nb = 0, epre = 0;
+    double be = 0, nb = 0, epre = 0, be2 = 0, fe = 0;
     struct timespec t0, t1;
     quiet_begin();
     clock_gettime(CLOCK_MONOTONIC, &t0);
@@ -473,7 +478,7 @@ double ref_time_symbol_chain(const float *snr_db, int n_snr, int n_frames, int f
             float sum = 0;
             for (int d = 0; d < D; ++d)
                 for (int j = 0; j < 96; ++j) sum += abs(creal(payload[d][j]) - creal(demod[d][j]));
-            be += sum; nb += 96 * D; epre += es;
+            be += sum; nb += 96 * D; epre += es; be2 += (double)sum * sum; fe += sum > 0;
         }
     }
     clock_gettime(CLOCK_MONOTONIC, &t1);
@@ -482,5 +487,6 @@ double ref_time_symbol_chain(const float *snr_db, int n_snr, int n_frames, int f
     Deallocate_Array_2D(rx_time, D); Deallocate_Array_2D(rx_freq, D);
     Deallocate_Array_2D(no_pilot, D); Deallocate_Array_2D(final, D); Deallocate_Array_2D(demod, D);
     if (acc3) { acc3[0] += be; acc3[1] += nb; acc3[2] += epre; }
+    if (acc3 && (flags & 4)) { acc3[3] += be2; acc3[4] += fe; }
     return (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
 }

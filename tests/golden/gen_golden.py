@@ -16,6 +16,9 @@ Outputs (all plain data, loadable with numpy allow_pickle=False / json):
   ref_genie_ls_curve.json  genie-timed symbol chain built from the reference's own ifft/fft/
                        Channel_Estimation (two separately noised LTF windows), real noise
                        sigma^2 = 0.4980 * 52/4096 / snr: pins symbol mode's LS estimator statistically
+  ref_symbol_chain_curve.json  the same chain entirely from the reference's stage functions and its
+                       gaussian_noise, 0..30 dB step 2, 2e6 frames at 8 / 10 dB and 1e7 at 12 dB (>= 1,000 bit
+                       errors each) with per-frame error statistics (frame-clustered BER variance)
 """
 from __future__ import annotations
 
@@ -135,6 +138,57 @@ def gen_genie(R: RefLib, frames: int = 20000, snrs=(0.0, 2.0, 4.0, 6.0)):
     (HERE / "ref_genie_ls_curve.json").write_text(json.dumps(meta, indent=1))
 
 
+CHAIN_SNRS = [float(x) for x in range(0, 31, 2)]            # bench.py's SNR grid
+CHAIN_FRAMES = 200_000                                     # per point: EVM to ~0.001 dB, BER down to 4 dB
+CHAIN_DEEP = {8.0: 2_000_000, 10.0: 2_000_000, 12.0: 10_000_000}   # >= 1,000 bit errors each
+CHAIN_JOB = 100_000                                        # frames per job, seeded by job index
+
+
+def _chain_worker(args):
+    snr, n, seed = args
+    return snr, RefLib().symbol_chain_stats(snr, n, seed).tolist()
+
+
+def chain_jobs(snrs=CHAIN_SNRS) -> list:
+    jobs = []
+    for snr in snrs:
+        n = CHAIN_DEEP.get(snr, CHAIN_FRAMES)
+        jobs += [(snr, CHAIN_JOB, 3000017 * (j + 1) + int(snr)) for j in range(n // CHAIN_JOB)]
+    return jobs
+
+
+def chain_rows(res: list) -> list:
+    """fixture rows from (snr, acc5) job results, summed in job order"""
+    acc = {}
+    for snr, a in res:
+        acc[snr] = [x + y for x, y in zip(acc.get(snr, [0.0] * 5), a)]
+    rows = []
+    for snr in sorted(acc):
+        be, nb, epre, be2, fe = acc[snr]
+        rows.append({"snr_db": snr, "frames": int(nb) // 192, "bits": int(nb), "bit_err": int(be),
+                     "evm_terms": int(nb) // 2, "sum_evm_pre": epre, "sum_frame_err_sq": int(be2),
+                     "frames_with_err": int(fe)})
+    return rows
+
+
+def gen_chain(procs: int):
+    """ref_symbol_chain_curve.json: the genie symbol chain built from the reference's own stage functions
+    (ref_harness.c ref_time_symbol_chain: QPSK_Modulator, ifft, gaussian_noise, Channel_Estimation, fft,
+    AGC_Receiver, QPSK_Demodulator -- OFDM.c:415-433, 320-339, 622-655, 830-850, 314-318, 852-908) over the
+    bench's SNR grid, with the per-frame error statistics that give the frame-clustered BER variance.
+    Jobs of CHAIN_JOB frames seeded 3000017 (j + 1) + snr, so the file does not depend on --procs."""
+    with mp.Pool(procs) as pool:
+        res = pool.map(_chain_worker, chain_jobs(), chunksize=1)     # job order: sums independent of --procs
+    rows = chain_rows(res)
+    meta = {"generator": f"tests/golden/gen_golden.py --only chain (jobs of {CHAIN_JOB} frames)",
+            "source": "reference OFDM.c stage functions (gcc -O2) composed as the genie symbol chain "
+                      "(oracle/ref_harness.c ref_time_symbol_chain, flags 4), real noise "
+                      "sigma^2 = 0.4980 * 52/4096 / 10^(snr/10), LCG rand hook",
+            "seeds": "job j of a point: noise 3000017 (j + 1) + snr, bits derived from it (RefLib.symbol_chain_stats)",
+            "rows": rows}
+    (HERE / "ref_symbol_chain_curve.json").write_text(json.dumps(meta, indent=1))
+
+
 MC_SNRS = list(range(0, 17)) + [18, 20, 22, 24, 26, 28, 30]
 MC_DEEP_SNRS = (11, 12, 13, 14, 15)     # the BER waterfall, where the curve is set by rare sync failures
 MC_DEEP_SCALE = {13: 4, 14: 4, 15: 4}   # x --mc-deep-trials where the 1e-3.5 .. 1e-5 crossings are pinned
@@ -209,7 +263,7 @@ def main():
     ap.add_argument("--mc-deep-trials", type=int, default=1_000_000)
     ap.add_argument("--procs", type=int, default=8)
     ap.add_argument("--skip-mc", action="store_true")
-    ap.add_argument("--only", choices=["genie", "mc"], help="regenerate one fixture only")
+    ap.add_argument("--only", choices=["genie", "mc", "chain"], help="regenerate one fixture only")
     a = ap.parse_args()
     build_ref()
     R = RefLib()
@@ -219,7 +273,10 @@ def main():
     if a.only == "mc":
         gen_mc(a.mc_trials, a.procs, a.mc_deep_trials)
         return
-    gen_fft(R); gen_tx(R); gen_rx(R); gen_kat(); gen_genie(R)
+    if a.only == "chain":
+        gen_chain(a.procs)
+        return
+    gen_fft(R); gen_tx(R); gen_rx(R); gen_kat(); gen_genie(R); gen_chain(a.procs)
     if not a.skip_mc:
         gen_mc(a.mc_trials, a.procs, a.mc_deep_trials)
     print("golden fixtures written to", HERE)

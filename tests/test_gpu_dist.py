@@ -2,6 +2,8 @@
 
 * C4's per-rank shard at its stated size (1e8 symbols/point over 8 ranks = 1.25e7 per rank) equals
   the sum of its two halves bit for bit (counter-range sharding of OFDM.c's trial loop :1195-1222).
+* C4's and C5's whole jobs, split 8 / 4 / 2 ways by shard_range and run rank after rank on this
+  device ("fake ranks"), sum to the single-range sweep bit for bit.
 * Two spawned processes on cuda:0 run Engine.symbol_sweep / sweep.reference_main on their shard
   and reduce through dist.allreduce_counters over gloo: bit-identical to one process.
 * torchrun launches bench.py as a fresh child, so init_process_group("nccl") and the RCCL
@@ -59,6 +61,25 @@ def test_c5_rank_shard_equals_halves(engine, pkg):
     assert np.array_equal(whole, halves)
     ber = whole[:, 3] / whole[:, 2]
     assert np.all(np.diff(ber[:8]) < 0)                 # BER falls with SNR (diversity-limited slope)
+
+
+@pytest.mark.parametrize("workload", ["c4", "c5"])
+def test_full_job_over_fake_ranks_equals_single_range(engine, pkg, workload):
+    """SURVEY §4 "fake 8 ranks": the WHOLE job of C4 (1e8 symbols/point = 5e7 frames, AWGN + LS) and of C5
+    (1e9 symbol-SNR evaluations = 3.125e7 frames, 4-tap Rayleigh + LS/ZF) split as dist.shard_range does
+    for 2, 4 and 8 ranks, the shards run one after another on this device and summed on the host: every
+    split equals the single-range sweep bit for bit (the sharded trial loop, /root/reference/src/OFDM.c:
+    1195-1222; the counters are integer sums of per-frame terms)."""
+    from ofdm_amd import dist as odist
+    frames_total = 100_000_000 // 2 if workload == "c4" else 1_000_000_000 // 16 // 2
+    cfg = pkg.make_cfg() if workload == "c4" else pkg.make_cfg(noise="real", channel="rayleigh4")
+    whole = engine.symbol_sweep(cfg, SNR, frames_total)
+    assert np.all(whole[:, 0] == frames_total) and np.all(whole[:, 2] == 192 * frames_total)
+    for world in (8, 4, 2):
+        parts = [engine.symbol_sweep(cfg, SNR, b - a, first_frame=a)
+                 for a, b in (odist.shard_range(frames_total, r, world) for r in range(world))]
+        assert np.array_equal(sum(parts), whole), world
+        assert all(not np.array_equal(p, parts[0]) for p in parts[1:])      # the shards are distinct streams
 
 
 def _sweep_worker(rank, world, port, n, out_path):

@@ -311,3 +311,37 @@ def test_ls_gpu_matches_reference_estimator_curve(engine, pkg):
             evm_ref = 10 * np.log10(r["sum_evm_pre"] / r["evm_terms"])
             evm = 10 * np.log10(row[7] / 2 ** 20 / row[6])
             assert abs(evm - evm_ref) < 0.05, (r["snr_db"], evm, evm_ref)
+
+
+def test_ls_gpu_matches_reference_stage_chain_to_30db(engine, pkg):
+    """The benchmarked c3 chain (real AWGN, LTF LS, slicer; the packed receiver) vs the symbol chain composed
+    from the reference's OWN stage functions and gaussian_noise (tests/golden/ref_symbol_chain_curve.json:
+    QPSK_Modulator, ifft, Channel_Estimation, fft, AGC_Receiver, QPSK_Demodulator; /root/reference/src/
+    OFDM.c:415-433, 314-339, 622-655, 830-908, 1044-1052, 1104-1161) over the bench's grid 0..30 dB:
+      * BER within 5 frame-clustered sigma wherever the reference counted errors -- 2e6 reference frames at
+        8 and 10 dB (1.7e5 and 4.4e3 bit errors), 1e7 at 12 dB (48) -- the reference's per-frame
+        error moments give both sides' variance;
+      * no more errors than the reference's rule-of-three bound where it counted none (14..30 dB);
+      * pooled pre-slicer EVM within 0.05 dB at every point (4 dB up: the pooled ZF EVM converges there)."""
+    import json
+    from conftest import GOLDEN
+    rows = json.loads((GOLDEN / "ref_symbol_chain_curve.json").read_text())["rows"]
+    n = 50_000_000
+    c = engine.symbol_sweep(pkg.make_cfg(), [r["snr_db"] for r in rows], n)
+    for r, row in zip(rows, c):
+        snr = r["snr_db"]
+        p, nb = row[3] / row[2], row[2]
+        if r["bit_err"]:
+            p_ref = r["bit_err"] / r["bits"]
+            m1 = r["bit_err"] / r["frames"]                       # per-frame errors: mean, second moment
+            m2 = r["sum_frame_err_sq"] / r["frames"]
+            var_ref = (m2 - m1 * m1) / r["frames"] / 192 ** 2
+            # the GPU's per-frame second moment at its own error rate, with the reference's cluster size
+            var_gpu = (r["sum_frame_err_sq"] / r["bit_err"]) * (row[3] / n) / n / 192 ** 2
+            assert abs(p - p_ref) < 5 * math.sqrt(var_ref + var_gpu), (snr, p, p_ref)
+        else:
+            assert p <= 3.0 / r["bits"], (snr, p)
+        if snr >= 4:
+            evm_ref = 10 * np.log10(r["sum_evm_pre"] / r["evm_terms"])
+            evm = 10 * np.log10(row[7] / 2 ** 20 / row[6])
+            assert abs(evm - evm_ref) < 0.05, (snr, evm, evm_ref)

@@ -148,3 +148,29 @@ def test_symbol_ls_pair_noise_matches_reference_estimator(oracle):
             evm_ref = 10 * np.log10(r["sum_evm_pre"] / r["evm_terms"])
             evm = 10 * np.log10(c[7] / 2 ** 20 / c[6])
             assert abs(evm - evm_ref) < 0.05, (r["snr_db"], evm, evm_ref)
+
+
+def _chain_rows():
+    return {r["snr_db"]: r for r in json.loads((GOLDEN / "ref_symbol_chain_curve.json").read_text())["rows"]}
+
+
+def test_symbol_chain_fixture_reproduces(reflib):
+    """tests/golden/ref_symbol_chain_curve.json is what gen_golden.py --only chain writes: its 30 dB row
+    regenerated here job by job (the reference's stage functions, ref_time_symbol_chain) is identical."""
+    import sys
+    sys.path.insert(0, str(GOLDEN))
+    import gen_golden
+    res = [(snr, reflib.symbol_chain_stats(snr, n, seed).tolist()) for snr, n, seed in gen_golden.chain_jobs([30.0])]
+    assert gen_golden.chain_rows(res) == [_chain_rows()[30.0]]
+
+
+def test_oracle_evm_matches_reference_chain_to_30db(oracle):
+    """Pre-slicer EVM of the oracle's LS symbol chain vs the reference's stage-function chain
+    (ref_symbol_chain_curve.json) from 8 to 30 dB: EVM ~ -(SNR + 2.2) dB, within 0.05 dB."""
+    rows = _chain_rows()
+    snrs = [8.0, 14.0, 20.0, 30.0]
+    cnt = oracle.symbol_sweep(oracle.cfg(), snrs, 0, 4000)
+    for s, c in zip(snrs, cnt):
+        evm_ref = 10 * np.log10(rows[s]["sum_evm_pre"] / rows[s]["evm_terms"])
+        evm = 10 * np.log10(c[7] / 2 ** 20 / c[6])
+        assert abs(evm - evm_ref) < 0.05, (s, evm, evm_ref)
