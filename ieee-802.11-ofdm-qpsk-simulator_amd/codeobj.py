@@ -28,7 +28,7 @@ WORKLOAD_KERNELS = {
     "c4": ("rx_pack_kernelILi2ELi0ELi0ELb0E",),
     "c5": ("rx_pack_kernelILi2ELi0ELi1ELb0E",),
     "c2": ("rx_pack_kernelILi0ELi0ELi0ELb0E",),
-    "frame": ("frame_sync_kernel", "frame_sym_kernelILb0E"),
+    "frame": ("frame_sync_kernelILi2ELi3008E", "frame_sym_kernelILb0E"),
 }
 
 
@@ -46,8 +46,9 @@ def _bundles(blob: bytes):
         pos = blob.find(BUNDLE_MAGIC, o)
 
 
-def _elf_symbols(elf: bytes):
-    """{name: bytes} of every sized FUNC / OBJECT symbol of an ELF64 little-endian code object."""
+def _elf_symbols(elf: bytes, with_type: bool = False):
+    """{name: bytes} (with_type: {name: (STT type, bytes)}) of every sized FUNC / OBJECT symbol of an ELF64
+    little-endian code object."""
     if elf[:4] != b"\x7fELF" or elf[4] != 2:
         return {}
     shoff, = struct.unpack_from("<Q", elf, 0x28)
@@ -66,18 +67,19 @@ def _elf_symbols(elf: bytes):
             name = elf[so:elf.index(b"\0", so)].decode()
             sec = secs[shndx]                # sh_addr, sh_offset: file offset of the symbol's bytes
             start = sec[4] + (value - sec[3])
-            out[name] = elf[start:start + size]
+            out[name] = (info & 0xF, elf[start:start + size]) if with_type else elf[start:start + size]
     return out
 
 
 @lru_cache(maxsize=8)
-def _symbols(path: str, mtime: float) -> dict:
+def _code_objects(path: str, mtime: float) -> list:
+    """[{name: (STT type, bytes)}] per gfx950 code object (one per translation unit)"""
     blob = Path(path).read_bytes()
-    syms = {}
-    for triple, body in _bundles(blob):
-        if triple.endswith(TARGET):
-            syms.update(_elf_symbols(body))
-    return syms
+    return [_elf_symbols(body, with_type=True) for triple, body in _bundles(blob) if triple.endswith(TARGET)]
+
+
+def _symbols(path: str, mtime: float) -> dict:
+    return {n: b for co in _code_objects(path, mtime) for n, (_, b) in co.items()}
 
 
 def kernel_symbols(lib_path) -> dict:
@@ -86,17 +88,27 @@ def kernel_symbols(lib_path) -> dict:
     return _symbols(str(p), p.stat().st_mtime)
 
 
+STT_FUNC = 2
+
+
 def kernel_build_id(lib_path, fragments) -> str | None:
     """sha256 (first 16 hex digits) over the code and kernel descriptor (its code-entry offset zeroed) of every
-    kernel whose mangled name contains one of `fragments`; None when no kernel matches."""
-    syms = kernel_symbols(lib_path)
-    names = sorted(n for n in syms if any(re.search(re.escape(f), n) for f in fragments))
-    if not names:
-        return None
+    kernel whose mangled name contains one of `fragments`, and over every non-kernel function of the code objects
+    holding them (a device function the compiler did not inline is code the kernel runs: ADVICE r3); None when no
+    kernel matches.  The kernels' constant data is their descriptors (.rodata holds nothing else here)."""
+    p = Path(lib_path)
     h = hashlib.sha256()
-    for n in names:
-        h.update(n.encode() + b"\0" + _layout_free(n, syms[n]))
-    return h.hexdigest()[:16]
+    found = False
+    for co in _code_objects(str(p), p.stat().st_mtime):
+        names = sorted(n for n in co if any(re.search(re.escape(f), n) for f in fragments))
+        if not names:
+            continue
+        found = True
+        callees = sorted(n for n, (t, _) in co.items()
+                         if t == STT_FUNC and not n.endswith(".kd") and n + ".kd" not in co)
+        for n in names + callees:
+            h.update(n.encode() + b"\0" + _layout_free(n, co[n][1]))
+    return h.hexdigest()[:16] if found else None
 
 
 def _layout_free(name: str, body: bytes) -> bytes:

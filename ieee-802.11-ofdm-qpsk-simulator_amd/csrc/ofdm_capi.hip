@@ -342,6 +342,12 @@ int ofdm_set_next_tx(ofdm_ctx *ctx, const ofdm_cfg *cfg, uint64_t first_frame, i
     return OFDM_OK;
 }
 
+// [a, a + na) and [b, b + nb) share a byte
+static bool overlaps(const void *a, int64_t na, const void *b, int64_t nb) {
+    const uintptr_t x = (uintptr_t)a, y = (uintptr_t)b;
+    return na > 0 && nb > 0 && x < y + (uintptr_t)nb && y < x + (uintptr_t)na;
+}
+
 // own_tx: the call also builds the batch it reads (ofdm_txrx_frames), d_tx / d_bits then being writable
 static int rx_common(Ctx *c, const ofdm_cfg *cfg, const void *d_tx, const void *d_bits, uint64_t first_frame,
                      int64_t n_frames, const double *snr_db, int n_snr, void *d_counters, void *d_eq, void *d_dbits,
@@ -356,6 +362,19 @@ static int rx_common(Ctx *c, const ofdm_cfg *cfg, const void *d_tx, const void *
     if (n_frames > MAX_BATCH_FRAMES) return set_error(OFDM_E_ARG, "n_frames > %lld per batch", (long long)MAX_BATCH_FRAMES);
     const bool dump = d_eq || d_dbits;
     if (dump && (!d_eq || !d_dbits)) return set_error(OFDM_E_ARG, "dump needs both d_eq and d_dbits");
+    // a pending next batch is written while this call reads (or, fused, builds) its own: the two must not share a
+    // byte (groups of one launch would race on it)
+    if (c->nx_pending && n_frames > 0) {
+        int64_t otx, obits, ntx, nbits;
+        ofdm_tx_bytes(n_frames, &otx, &obits);
+        ofdm_tx_bytes(c->nx_n, &ntx, &nbits);
+        const void *own[2] = {d_tx, d_bits}, *nx[2] = {c->nx_tx, c->nx_bits};
+        const int64_t osz[2] = {otx, obits}, nsz[2] = {ntx, nbits};
+        for (int i = 0; i < 2; ++i)
+            for (int j = 0; j < 2; ++j)
+                if (overlaps(own[i], osz[i], nx[j], nsz[j]))
+                    return set_error(OFDM_E_ARG, "the pending ofdm_set_next_tx batch overlaps this call's batch");
+    }
     // a pending ofdm_set_next_tx batch: fused into the packed receiver's group prologues when this call
     // launches it, otherwise built by the Tx kernel right here (same stream, so it is ready in either case
     // once this call's work is)

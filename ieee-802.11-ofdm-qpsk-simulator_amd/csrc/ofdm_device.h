@@ -121,6 +121,33 @@ __device__ __forceinline__ uint4 philox10_c2(const PhiloxHead &h, uint32_t c2, c
     return make_uint4(c0, c1, c2, c3);
 }
 
+// philox10_c2 for NB blocks at once with the round keys in VGPRs (same outputs), round-major: the NB blocks'
+// multiply chains interleave (ILP 2 NB) instead of running one block after another
+template <int NB>
+__device__ __forceinline__ void philox10_c2_multi(const PhiloxHead &h, const uint32_t (&c2in)[NB], const PhiloxKeysV &k,
+                                                  uint4 (&out)[NB]) {
+    uint32_t c0[NB], c1[NB], c2[NB], c3[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const uint64_t p1r = (uint64_t)PHILOX_M1 * c2in[b];
+        c0[b] = __builtin_amdgcn_bitop3_b32((uint32_t)(p1r >> 32), h.c1, k.k0[0], 0x96);
+        c1[b] = (uint32_t)p1r; c2[b] = h.n2; c3[b] = h.c3;
+    }
+#pragma unroll
+    for (int r = 1; r < 10; ++r) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            const uint64_t p0 = (uint64_t)PHILOX_M0 * c0[b];
+            const uint64_t p1 = (uint64_t)PHILOX_M1 * c2[b];
+            const uint32_t n0 = __builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c1[b], k.k0[r], 0x96);
+            const uint32_t n2 = __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c3[b], k.k1[r], 0x96);
+            c0[b] = n0; c1[b] = (uint32_t)p1; c2[b] = n2; c3[b] = (uint32_t)p0;
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) out[b] = make_uint4(c0[b], c1[b], c2[b], c3[b]);
+}
+
 // philox10_c2 for NB blocks at once (same outputs), round keys in VGPRs: a v_bitop3_b32 with an SGPR
 // operand issues at the slow rate, one with three VGPRs at the fast rate.  The keys
 // are moved to VGPRs once and advanced round by round with v_add (literal W0 / W1), shared by the NB

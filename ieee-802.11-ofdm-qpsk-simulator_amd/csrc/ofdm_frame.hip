@@ -84,6 +84,7 @@ struct FrameArgs {
     int4 *info;                     // [n_items]: packet_idx, sync_fail, oob, rx_start
     int32_t add_totals;             // 1 on the last chunk: add frames / symbols / bits / terms
     unsigned long long *work;       // sync kernel: items handed out past the first gridDim.x (zeroed per launch)
+    int32_t region_floats;          // LDS floats per wave (wave_region_floats)
 };
 
 #ifdef OFDM_FRAME_STAMPS   // diagnostic build: s_memtime per phase, summed over the grid
@@ -320,6 +321,7 @@ __device__ __forceinline__ int needed_k(int j) {
 #ifndef FRAME_SYNC_WAVES
 #define FRAME_SYNC_WAVES 4
 #endif
+constexpr int SYM_THREADS = 256;    // frame_sym_kernel block: its items per block set the hand-off tile
 constexpr int SYNC_WAVES = FRAME_SYNC_WAVES;
 constexpr int SYNC_THREADS = 64 * SYNC_WAVES;
 constexpr int IMT_EXT = 128;         // table slack past one waveform copy: a lane's longest contiguous read
@@ -336,11 +338,79 @@ static_assert(64 * 2 * DET_MAX_CHUNK + 47 >= CAP_ABS_MAX, "two detection rounds 
 #ifndef FRAME_ITEM_RUN
 #define FRAME_ITEM_RUN 4            // items per hand-out of the sync kernel's work counter (per wave)
 #endif
+#ifndef FRAME_LAZY
+#define FRAME_LAZY 1        // lazy capture + detection (see frame_sync_kernel; A/B: +5.3 %, profiles/r03/ab_n/)
+#endif
+#ifndef FRAME_R1_SPREAD
+#define FRAME_R1_SPREAD 1   // round 1 in one 16-position batch where spread chunks allow (A/B option)
+#endif
+#ifndef FRAME_LAZY_C0
+#define FRAME_LAZY_C0 31    // round-0 positions per lane when lazy (two 16-position batches)
+#endif
+// Detection geometry for Lc = cap_len - 47 positions: R rounds of 64 lanes, round 0 c0 positions per lane over
+// [0, B1 = 64 c0), round 1 c1 per lane from B1 (chunks odd: the lanes' LDS reads fall in distinct banks)
+struct DetGeom {
+    int c0, c1, x1, B1, R;
+    // first position of lane l's round-1 chunk, relative to B1
+    __host__ __device__ int r1_start(int l) const { return l * c1 + ((l * x1) >> 6); }
+    __host__ __device__ static DetGeom of(int Lc) {
+        DetGeom g{};
+#if FRAME_LAZY
+        // Lazy: round 0 covers the first 64 FRAME_LAZY_C0 positions (the reference capture: 1984 of 2961), and
+        // only the capture samples round 0 reads are generated before it; when round 0 alone decides
+        // Packet_Selection and the matched filter reads inside that part, the rest of the capture and round 1
+        // are skipped (same packet_idx, same frame: see the selection in frame_sync_kernel).
+        g.c0 = Lc > 64 * FRAME_LAZY_C0 ? FRAME_LAZY_C0 : (((Lc + 63) / 64) | 1);
+        g.B1 = 64 * g.c0;
+        g.R = Lc > g.B1 ? 2 : 1;
+        // round 1: a uniform odd chunk, or -- when that saves a 16-position batch (the reference capture: 977
+        // positions = 64 x 15 + 17, one batch instead of two of chunk 17) -- c1 positions per lane plus one more
+        // on x1 lanes spread evenly (lane l starts at B1 + l c1 + floor(l x1 / 64): at most 2-way bank conflicts)
+        g.c1 = g.R == 2 ? (((Lc - g.B1 + 63) / 64) | 1) : g.c0;
+        g.x1 = 0;
+        if (g.R == 2) {
+            const int c1b = (Lc - g.B1) / 64, r1 = (Lc - g.B1) - 64 * c1b;
+            if (FRAME_R1_SPREAD && (c1b + (r1 > 0) + DET_B - 1) / DET_B < (g.c1 + DET_B - 1) / DET_B) {
+                g.c1 = c1b;
+                g.x1 = r1;
+            }
+        }
+#else
+        // one round for the reference capture (chunk 47)
+        g.R = (Lc + 64 * DET_MAX_CHUNK - 1) / (64 * DET_MAX_CHUNK);
+        g.c0 = ((Lc + 64 * g.R - 1) / (64 * g.R)) | 1;
+        g.c1 = g.c0;
+        g.B1 = 64 * g.c0;
+        g.x1 = 0;
+#endif
+        return g;
+    }
+    // the last capture sample (relative to the capture start) a detection round's register blocks load: every
+    // active lane loads ceil(chunk / DET_B) + 3 blocks of DET_B from its first position, the last active lane's
+    // reaching furthest (up to 3 blocks past the capture)
+    __host__ __device__ int max_read(int Lc) const {
+        int m = 0;
+        const int nb0 = (c0 + DET_B - 1) / DET_B, l0 = min(63, (Lc - 1) / c0);
+        m = max(m, l0 * c0 + DET_B * (nb0 + 3) - 1);
+        if (R == 2) {
+            const int nb1 = (c1 + (x1 > 0) + DET_B - 1) / DET_B;
+            int l1 = 63;
+            while (l1 > 0 && B1 + r1_start(l1) >= Lc) --l1;
+            m = max(m, B1 + r1_start(l1) + DET_B * (nb1 + 3) - 1);
+        }
+        return m;
+    }
+};
 // per-SNR block accumulators: sync failures, OOB reads (and, with word_stats, the word-length min / max)
 __host__ __device__ inline int acc_slots(int word_stats) { return word_stats ? 4 : 2; }
-// capture region (floats): cap_len + 8, the capture starting at float (rx_start & 3) so that every Philox
-// block of 4 samples is one 16-byte aligned ds_write_b128; a multiple of 4 floats (16-byte aligned regions)
-__host__ __device__ inline int cap_region(int cap_len) { return (cap_len + 8 + 3) & ~3; }
+// capture region (floats), a multiple of 4 (16-byte aligned regions): the capture starts at float (rx_start & 3)
+// so that every Philox block of 4 samples is one 16-byte aligned ds_write_b128; the region holds the capture's
+// L + 8 floats, the detection blocks the last active lane loads (DetGeom::max_read) and the matched-filter runs'
+// last window (a run cut short at the end of a needed range reads up to L + 5, i.e. float L + 8)
+__host__ __device__ inline int cap_region(int cap_len) {
+    const int det = 3 + DetGeom::of(cap_len - 47).max_read(cap_len - 47) + 1;
+    return (max(cap_len + 9, det) + 3) & ~3;
+}
 // The filtered frame fr[] (float2, indexed by frame sample) goes into the part of the capture region the
 // matched filter does not read: it reads 2 nfr + 19 floats, so the unread prefix or suffix holds the 2 nfr
 // floats of fr[] whenever the region has 6 nfr + 24.  Shorter user captures get fr[] after the region.
@@ -363,11 +433,14 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 // x mod the table period for 0 <= x < 2^14 (q = floor(x / period) by multiply-high: exact there)
-template <typename A>
-__device__ __forceinline__ int im_mod(const A &a, int x) {
-    const uint32_t q = __umulhi((uint32_t)x, a.im_magic);
-    return x - (int)(q * (uint32_t)a.im_period);
-}
+struct ImMod {
+    int period;
+    uint32_t magic;      // ceil(2^32 / period)
+    __device__ __forceinline__ int operator()(int x) const {
+        const uint32_t q = __umulhi((uint32_t)x, magic);
+        return x - (int)(q * (uint32_t)period);
+    }
+};
 
 // N (odd) contiguous LDS floats x[k] = p[s + k] as (N - 1) / 2 ds_read_b64 + 1 ds_read_b32; ODD = s & 1 (uniform
 // per item), so the pairs are 8-byte aligned
@@ -385,83 +458,85 @@ __device__ __forceinline__ void lds_readn(const float *p, int s, float (&x)[N]) 
     if constexpr (!ODD) x[N - 1] = p[s + N - 1];
 }
 
-#ifndef FRAME_LAZY
-#define FRAME_LAZY 1        // lazy capture + detection (see frame_sync_kernel; A/B: +5.3 %, profiles/r03/ab_n/)
-#endif
-#ifndef FRAME_R1_SPREAD
-#define FRAME_R1_SPREAD 1   // round 1 in one 16-position batch where spread chunks allow (A/B option)
-#endif
-#ifndef FRAME_LAZY_C0
-#define FRAME_LAZY_C0 31    // round-0 positions per lane when lazy (two 16-position batches)
-#endif
 
 // Capture Philox blocks bs..be (block b = waveform samples 4b..4b+3; b0 = the capture's first block) into the
 // wave's region: the real parts of the clean waveform plus real AWGN (OFDM.c:622-655, D7).
 template <typename A>
-__device__ __forceinline__ void capture_blocks(const A &a, float *rbase, int b0, int bs, int be, int lane, uint32_t t_lo,
-                                               uint32_t t_hi, uint32_t qs, float sigma) {
+__device__ __forceinline__ void capture_blocks(const A &a, int wave_len, float *rbase, int b0, int bs, int be, int lane,
+                                               uint32_t t_lo, uint32_t t_hi, uint32_t qs, float sigma) {
     const PhiloxHead hd = philox_head(t_lo, t_hi, STREAM_NOISE | qs, a.k1);
     const float Ksig = noise_k(sigma);
-#ifndef FRAME_CAP_SKEYS
     // round keys in VGPRs: each round's two v_bitop3_b32 issue at the fast rate (an SGPR operand makes
     // them slow-class); 20 VGPRs for the capture loop only
     PhiloxKeysV vk;
     vk.init(a.k0, a.k1);
-#endif
     // Gaussian k of the trial's stream goes to waveform sample k (as if Transmission_Over_Air had drawn
     // the whole waveform); only the captured samples are ever evaluated.  The waveform is FR_REPS
     // copies of one filtered frame (OFDM.c:607-612): sample k is sample k mod nfilt of the first copy
     // (7.8 KB, L1-resident).  bm = the block's index within the copy.
-    const uint32_t pb = (uint32_t)(a.wave_len / (4 * FR_REPS)), nb_wave = (uint32_t)(a.wave_len / 4);
+    const uint32_t pb = (uint32_t)(wave_len / (4 * FR_REPS)), nb_wave = (uint32_t)(wave_len / 4);
     uint32_t bm = (uint32_t)(bs + lane) % pb;
+    const bool real = a.noise == OFDM_NOISE_REAL;        // real-only AWGN (D7), or noiseless
 #ifndef FRAME_CAP_U
 #define FRAME_CAP_U 4   // Philox blocks per lane per pass: the lazy capture's 8 + 4 blocks in passes of 4 (A/B: +1.3 % over 6, = 8)
 #endif
-    for (int bb = bs + lane; bb <= be; bb += FRAME_CAP_U * 64) {
+    // Passes are uniform over the wave and free of per-lane control flow: every lane loads, draws and combines
+    // its FRAME_CAP_U blocks (a lane past `be` computes a block it does not store), so the blocks' Philox rounds
+    // and Box-Muller transcendentals interleave (ILP 2 FRAME_CAP_U in the multiply chains)
+    for (int p0 = bs; p0 <= be; p0 += FRAME_CAP_U * 64) {
+        const int bb = p0 + lane;
         float4 v[FRAME_CAP_U];
 #pragma unroll
         for (int u = 0; u < FRAME_CAP_U; ++u) {
             const int b = bb + 64 * u;
-            const float4 *s4 = reinterpret_cast<const float4 *>(a.wave + 4 * bm);
-            const bool in = b <= be && (uint32_t)b < nb_wave;
-            const float4 lo = in ? s4[0] : make_float4(0.f, 0.f, 0.f, 0.f);
-            const float4 hi = in ? s4[1] : make_float4(0.f, 0.f, 0.f, 0.f);
-            v[u] = make_float4(lo.x, lo.z, hi.x, hi.z);
+            const float4 *s4 = reinterpret_cast<const float4 *>(a.wave + 4 * bm);   // bm < pb: in the waveform
+            const float4 lo = s4[0], hi = s4[1];
+            const bool in = (uint32_t)b < nb_wave;                     // past the waveform's end: zeros
+            v[u] = in ? make_float4(lo.x, lo.z, hi.x, hi.z) : make_float4(0.f, 0.f, 0.f, 0.f);
             bm = bm + 64 >= pb ? bm + 64 - pb : bm + 64;           // (bm + 64) mod pb (pb > 64)
         }
+        if (real) {         // sigma z = sqrt(K log2 u1) (cos | sin 2 pi u2) per pair
+            uint32_t c2[FRAME_CAP_U];
+            uint4 o[FRAME_CAP_U];
 #pragma unroll
-        for (int u = 0; u < FRAME_CAP_U; ++u) {
-            const int b = bb + 64 * u;
-            if (b > be) break;
-            float4 w = v[u];
-            if (a.noise == OFDM_NOISE_REAL) {   // real-only (D7): sigma z = sqrt(K log2 u1) (cos | sin)
-#ifndef FRAME_CAP_SKEYS
-                const Noise4 nz = noise4_of(philox10_c2(hd, (uint32_t)b, vk), Ksig);
-#else
-                const Noise4 nz = noise4_of(philox10_c2(hd, (uint32_t)b, a.k0, a.k1), Ksig);
-#endif
-                w.x = fmaf(nz.r0, nz.c0, w.x); w.y = fmaf(nz.r0, nz.s0, w.y);
-                w.z = fmaf(nz.r1, nz.c1, w.z); w.w = fmaf(nz.r1, nz.s1, w.w);
+            for (int u = 0; u < FRAME_CAP_U; ++u) c2[u] = (uint32_t)(bb + 64 * u);
+            philox10_c2_multi(hd, c2, vk, o);
+#pragma unroll
+            for (int u = 0; u < FRAME_CAP_U; ++u) {
+                const Noise4 nz = noise4_of(o[u], Ksig);
+                v[u].x = fmaf(nz.r0, nz.c0, v[u].x); v[u].y = fmaf(nz.r0, nz.s0, v[u].y);
+                v[u].z = fmaf(nz.r1, nz.c1, v[u].z); v[u].w = fmaf(nz.r1, nz.s1, v[u].w);
             }
-            // samples of the block outside [0, L) land in the region's slack, never read as capture
-            *reinterpret_cast<float4 *>(rbase + 4 * (b - b0)) = w;
         }
+        // samples of the block outside [0, L) land in the region's slack, never read as capture
+#pragma unroll
+        for (int u = 0; u < FRAME_CAP_U; ++u)
+            if (bb + 64 * u <= be) *reinterpret_cast<float4 *>(rbase + 4 * (bb + 64 * u - b0)) = v[u];
     }
 }
 
 #ifndef FRAME_SYNC_MINW
 #define FRAME_SYNC_MINW 3   // waves per SIMD the VGPR budget targets (LDS holds 3 blocks of 4 waves per CU)
 #endif
+// FIX_ND, FIX_CAP > 0: the launch geometry as compile-time constants -- n_data data symbols per frame, captures of
+// FIX_CAP samples generated from the waveform (no external capture, no dumps, no word-length statistics): the
+// reference message's sweep, with the detection rounds, table period, matched-filter runs and hand-off layout
+// folded by the compiler.  0, 0: everything from the arguments (any message, user captures, the parity dumps).
+template <int FIX_ND, int FIX_CAP>
 __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kernel(FrameArgs a) {
+    constexpr bool FIX = FIX_ND > 0;
+    static_assert(FIX == (FIX_CAP > 0), "both or neither");
     extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
-    const int L = a.cap_len, Lc = L - 47;       // Packet_Detection length (OFDM.c:663)
-    const int nfr = fr_len(a.n_data);
-    const int ns = acc_slots(a.word_stats);
+    const int L = FIX ? FIX_CAP : a.cap_len, Lc = L - 47;       // Packet_Detection length (OFDM.c:663)
+    const int nfr = fr_len(FIX ? FIX_ND : a.n_data);
+    const int ns = acc_slots(!FIX && a.word_stats);
+    const int imt_len = FIX ? wave_len_for(FIX_ND) / FR_REPS + IMT_EXT : a.imt_len;
     unsigned long long *acc = smem;                                           // [n_snr][ns]
     float *imt = reinterpret_cast<float *>(acc + a.n_snr * ns);              // imaginary parts, [imt_len]
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    float *rbase = imt + ((a.imt_len + 3) & ~3) + wv * wave_region_floats(L, a.n_data);
-    float2 *const fr_sep = reinterpret_cast<float2 *>(rbase + cap_region(L));   // when !fr_in_capture
+    float *rbase = imt + ((imt_len + 3) & ~3) + wv * (FIX ? wave_region_floats(FIX_CAP, FIX_ND) : a.region_floats);
+    // fr[] after the capture region when !fr_in_capture (the region then ends with its 2 nfr floats)
+    float2 *const fr_sep = reinterpret_cast<float2 *>(rbase + (FIX ? cap_region(FIX_CAP) : a.region_floats - 2 * nfr));
     for (int i = threadIdx.x; i < a.n_snr * ns; i += SYNC_THREADS) {
         const int k = i % ns;
         acc[i] = k == 2 ? (unsigned long long)INT64_MAX : k == 3 ? (unsigned long long)INT64_MIN : 0ull;
@@ -469,39 +544,19 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
     // the table: waveform mode imt[k] = Im wave[k mod nfilt] (every capture sample n reads imt[(rx_start + n)
     // mod nfilt]; a lane's contiguous reads start below nfilt and run at most IMT_EXT past it); an external
     // capture (ofdm_receiver, one item) its own imaginary parts, imt[n] = Im ext[n], zero past L
-    for (int k = threadIdx.x; k < a.imt_len; k += SYNC_THREADS)
-        imt[k] = a.ext ? (k < L ? a.ext[k].y : 0.f) : a.wave[k % a.im_period].y;
+    for (int k = threadIdx.x; k < imt_len; k += SYNC_THREADS)
+        imt[k] = !FIX && a.ext ? (k < L ? a.ext[k].y : 0.f) : a.wave[k % (FIX ? imt_len - IMT_EXT : a.im_period)].y;
     __syncthreads();
     const int lane = threadIdx.x & 63;
 #ifdef OFDM_FRAME_STAMPS
     unsigned long long stamp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long stamp_t = __builtin_amdgcn_s_memtime();
 #endif
-    // detection geometry: R rounds of 64 lanes, round 0 c0 positions per lane over [0, B1 = 64 c0), round 1 c1
-    // per lane from B1 (chunks odd: the lanes' LDS reads fall in distinct banks)
-#if FRAME_LAZY
-    // Lazy: round 0 covers the first 64 FRAME_LAZY_C0 positions (the reference capture: 1984 of 2961), and only
-    // the capture samples round 0 reads are generated before it; when round 0 alone decides Packet_Selection and
-    // the matched filter reads inside that part, the rest of the capture and round 1 are skipped (same
-    // packet_idx, same frame: see the selection below).
-    const int c0 = Lc > 64 * FRAME_LAZY_C0 ? FRAME_LAZY_C0 : (((Lc + 63) / 64) | 1);
-    const int B1 = 64 * c0;
-    const int R = Lc > B1 ? 2 : 1;
-    // round 1: a uniform odd chunk, or -- when that saves a 16-position batch (the reference capture: 977
-    // positions = 64 x 15 + 17, one batch instead of two of chunk 17) -- c1 positions per lane plus one more on
-    // x1 lanes spread evenly (lane l starts at B1 + l c1 + floor(l x1 / 64): at most 2-way LDS bank conflicts)
-    int c1 = R == 2 ? (((Lc - B1 + 63) / 64) | 1) : c0, x1 = 0;
-    if (R == 2) {
-        const int c1b = (Lc - B1) / 64, r1 = (Lc - B1) - 64 * c1b;
-        if (FRAME_R1_SPREAD && (c1b + (r1 > 0) + DET_B - 1) / DET_B < (c1 + DET_B - 1) / DET_B) { c1 = c1b; x1 = r1; }
-    }
-#else
-    // one round for the reference capture (chunk 47)
-    const int R = (Lc + 64 * DET_MAX_CHUNK - 1) / (64 * DET_MAX_CHUNK);
-    const int c0 = ((Lc + 64 * R - 1) / (64 * R)) | 1, c1 = c0, B1 = 64 * c0, x1 = 0;
-#endif
-    // first position of lane l's round-1 chunk, relative to B1
-    auto r1_start = [c1, x1](int l) { return l * c1 + ((l * x1) >> 6); };
+    // detection geometry (DetGeom): R rounds of 64 lanes, c0 positions per lane in round 0, c1 (+ 1 on x1 lanes)
+    // in round 1 from B1
+    const DetGeom dg = DetGeom::of(Lc);
+    const int c0 = dg.c0, c1 = dg.c1, x1 = dg.x1, B1 = dg.B1, R = dg.R;
+    auto r1_start = [c1, x1](int l) { return l * c1 + ((l * x1) >> 6); };    // DetGeom::r1_start
     // Items go out in runs of FRAME_ITEM_RUN per wave: wave gw starts with run gw, the runs past the first
     // gridDim.x * SYNC_WAVES come from a per-launch atomic counter, so waves that run fast take more runs.
     // Lane 0 fetches the next run at the first item of the current one (its wait is paid once per run).
@@ -515,6 +570,16 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
         KArgs *ap = (KArgs *)__builtin_amdgcn_kernarg_segment_ptr();
         asm volatile("" : "+s"(ap));
         KArgs &a = *ap;
+        // the geometry: compile-time constants (FIX), or re-read per item with the arguments
+        const int n_data = FIX ? FIX_ND : a.n_data;
+        const int wave_len = FIX ? wave_len_for(FIX_ND) : a.wave_len;
+        const bool word_stats = !FIX && a.word_stats;
+        // the imaginary-part table: period nfilt (one waveform copy) for generated captures, 2^30 for an external one
+        const ImMod im_mod = FIX ? ImMod{wave_len_for(FIX_ND) / FR_REPS,
+                                         (uint32_t)((((uint64_t)1 << 32) + wave_len_for(FIX_ND) / FR_REPS - 1) /
+                                                    (wave_len_for(FIX_ND) / FR_REPS))}
+                                 : ImMod{a.im_period, a.im_magic};
+        const bool fr_in_cap = FIX ? fr_in_capture(FIX_CAP, FIX_ND) : a.fr_in_cap;
         if (lane == 0 && i == run_end - FRAME_ITEM_RUN) nxt = nwaves + (int)atomicAdd(a.work, 1ull);
         const int64_t g = a.item0 + i;
         int q;
@@ -531,22 +596,22 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
         const uint32_t t_lo = (uint32_t)t, t_hi = (uint32_t)(t >> 32), qs = (uint32_t)(a.q_base + q);
         const float sigma = a.sigma[q];
         const bool first_item = g == 0;
-        const bool ext = a.ext && first_item;
+        const bool ext = !FIX && a.ext && first_item;
         // ---- capture window (OFDM.c:945-955) + AWGN: the real parts only ----
         int rx_start = a.fixed_start;
         if (rx_start < 0) {
             const uint4 o = philox10(t_lo, t_hi, 0u, STREAM_START | qs, a.k0, a.k1);
-            rx_start = (int)(o.x % (uint32_t)(a.wave_len - L));
+            rx_start = (int)(o.x % (uint32_t)(wave_len - L));
         }
         rx_start = __builtin_amdgcn_readfirstlane(rx_start);     // uniform: the capture geometry in SGPRs
         const int off = rx_start & 3;
         const float *r = rbase + off;                       // r[n] = Re capture sample n
         // Im capture sample n = imt[im0 + n] reduced mod the period (a.im_period: nfilt, or 2^30 for ext)
-        const int im0 = ext ? 0 : im_mod(a, rx_start);
+        const int im0 = ext ? 0 : im_mod(rx_start);
         // lazy capture + detection (FRAME_LAZY): not for external captures, dumps or the word-length report,
         // which read the whole capture
-        const bool lazy = FRAME_LAZY && !a.no_lazy && !ext && R == 2 && !a.word_stats && !a.dbg_corr &&
-                          !(a.dbg_frame && first_item);
+        const bool lazy = FRAME_LAZY && !a.no_lazy && !ext && R == 2 && !word_stats &&
+                          (FIX || (!a.dbg_corr && !(a.dbg_frame && first_item)));
         int b1s = 0;                                         // last Philox block generated
         if (ext) {
             for (int n = lane; n < L; n += 64) rbase[off + n] = a.ext[n].x;
@@ -554,7 +619,7 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
             // lazy: the blocks of capture samples [0, B1 + 47) first (round 0 reads them), the rest on demand
             const int b0 = rx_start >> 2, b1 = (rx_start + L - 1) >> 2;
             b1s = lazy ? min((rx_start + B1 + 46) >> 2, b1) : b1;
-            capture_blocks(a, rbase, b0, b0, b1s, lane, t_lo, t_hi, qs, sigma);
+            capture_blocks(a, wave_len, rbase, b0, b0, b1s, lane, t_lo, t_hi, qs, sigma);
         }
         wave_lds_sync();
         FR_STAMP(0);                                           // capture + noise
@@ -564,7 +629,7 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
 
         // ---- Word_Optimization_Analysis(Rx_filter_signal) (OFDM.c:38-73, 962-967): the full RRC matched
         // filter of the capture, min / max over real and imaginary parts (opt-in) ----
-        if (a.word_stats) {
+        if (word_stats) {
             float mn = 1e9f, mx = -1e9f;
             for (int k = lx; k < L + 20; k += 64) {
                 float2 v = make_float2(0.f, 0.f);
@@ -572,7 +637,7 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
                 for (int j = 0; j < 21; ++j) {
                     const int m = k - j;
                     if (m >= 0 && m < L) {
-                        const int mi = im_mod(a, im0 + m);
+                        const int mi = im_mod(im0 + m);
                         v.x = fmaf(r[m], a.taps[j], v.x);
                         v.y = fmaf(imt[mi], a.taps[j], v.y);
                     }
@@ -603,8 +668,15 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
             const int n0 = rho ? B1 + r1_start(lx) : lx * c0, n1 = min(n0 + chunk, Lc);
             unsigned long long cmask = 0ull;
             if (rho < R && n0 < n1) {
-                const float *ti_ = imt + im_mod(a, im0 + n0);   // Im of sample n0 + k at ti_[k] (k < IMT_EXT)
-                const float *tr_ = r + n0;
+                // Im of sample n0 + k at ti_[k] (k < IMT_EXT), Re at tr_[k].  Both bases are held in one VGPR each
+                // (LDS address space, made opaque), so that every block read is a ds_read2_b32 off it with an
+                // immediate offset (< 1 KB) -- otherwise the compiler folds part of the table base into constants
+                // too large for the offset field and spends one v_add per read on addresses
+                using LdsF = const __attribute__((address_space(3))) float;
+                LdsF *ti_ = (LdsF *)(imt + im_mod(im0 + n0));
+                LdsF *tr_ = (LdsF *)(r + n0);
+                opaque(ti_);
+                opaque(tr_);
                 float sx = 0.f, sy = 0.f, pw = 0.f;
                 uint32_t mlo = 0u, mhi = 0u;
                 const int nbat = ((rho ? c1 + (x1 > 0) : c0) + DET_B - 1) / DET_B;   // uniform over the lanes
@@ -636,7 +708,7 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
                 // active lane runs the same ceil(chunk / DET_B) batches, positions past n1 are masked below
                 static_for<0, NB>([&](auto bc) {
                     constexpr int b = decltype(bc)::value;
-                    if (b < nbat) {                                // reads past the capture land in the slack
+                    if (b < nbat) {                                // reads past the capture stay in the region (cap_region)
                         load_blk(std::integral_constant<int, b + 3>{});
 #pragma unroll
                         for (int k = 0; k < DET_B; ++k) {
@@ -709,17 +781,18 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
         }
         if (R == 2 && !decided) {
             if (lazy) {                                          // the rest of the capture, then round 1
-                capture_blocks(a, rbase, rx_start >> 2, b1s + 1, (rx_start + L - 1) >> 2, lane, t_lo, t_hi, qs, sigma);
+                capture_blocks(a, wave_len, rbase, rx_start >> 2, b1s + 1, (rx_start + L - 1) >> 2, lane, t_lo, t_hi, qs,
+                               sigma);
                 wave_lds_sync();
             }
             detect(std::integral_constant<int, 1>{});
         }
-        if (a.dbg_corr && first_item) {             // Corr_Out for ofdm_receiver's parity dump
+        if (!FIX && a.dbg_corr && first_item) {     // Corr_Out for ofdm_receiver's parity dump
             for (int n = lx; n < Lc; n += 64) {
                 float sx = 0.f, sy = 0.f, pw = 0.f;
                 for (int k = 0; k < 32; ++k) {
-                    const float ux = r[n + k], uy = imt[im_mod(a, im0 + n + k)];
-                    const float vx = r[n + k + 16], vy = imt[im_mod(a, im0 + n + k + 16)];
+                    const float ux = r[n + k], uy = imt[im_mod(im0 + n + k)];
+                    const float vx = r[n + k + 16], vy = imt[im_mod(im0 + n + k + 16)];
                     sx += ux * vx - uy * vy;
                     sy += ux * vy + uy * vx;
                     pw += vx * vx + vy * vy;
@@ -760,7 +833,7 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
 
         // fr[] (float2) in the unread prefix [0, off + lo) or the unread suffix (off + hi, region) of the region
         float2 *fr = fr_sep;
-        if (a.fr_in_cap) {
+        if (fr_in_cap) {
             const int lo = max(p - 20, 0), hi = min(p + 2 * nfr - 2, L - 1);
             fr = off + lo >= 2 * nfr ? reinterpret_cast<float2 *>(rbase)
                                      : reinterpret_cast<float2 *>(rbase + ((off + hi + 2) & ~1));
@@ -770,7 +843,7 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
         // adjacent lanes read adjacent 8 B).  Only the 160 + 64 nd frame samples the receiver reads are
         // filtered (needed_k), all nfr for the single-capture dump.  The OOB flag is unchanged: the reference
         // reads past its buffer iff the last instant does, and the last sample is always needed. ----
-        const bool dbg = a.dbg_frame && first_item;
+        const bool dbg = !FIX && a.dbg_frame && first_item;
         bool oob_l = false;
         // the RRC taps are symmetric (h[t] = h[20 - t], OFDM.c:32; rrc_taps), so a window is 10 pair sums + the
         // centre tap: 11 FMAs per component instead of 21
@@ -795,7 +868,7 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
             float2 v = make_float2(0.f, 0.f);
             if (n >= 20 && n < L) {                              // all 21 taps inside the capture
                 float xr[21], xi[21];                            // x[20 - t] = sample n - t
-                const int si = im_mod(a, im0 + n - 20);
+                const int si = im_mod(im0 + n - 20);
                 if (par_r) lds_readn<1>(rbase, off + n - 20, xr); else lds_readn<0>(rbase, off + n - 20, xr);
                 if (par_i) lds_readn<1>(imt, si, xi); else lds_readn<0>(imt, si, xi);
                 v = make_float2(xr[10] * tv[10], xi[10] * tv[10]);
@@ -812,7 +885,7 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
                     const int m = n - tt;
                     const int mc = min(max(m, 0), L - 1);
                     const bool in = m >= 0 && m < L;
-                    const float xr = in ? r[mc] : 0.f, xi = in ? imt[im_mod(a, im0 + mc)] : 0.f;
+                    const float xr = in ? r[mc] : 0.f, xi = in ? imt[im_mod(im0 + mc)] : 0.f;
                     const float h = tv[tt <= 10 ? tt : 20 - tt];
                     v.x = fmaf(xr, h, v.x);
                     v.y = fmaf(xi, h, v.y);
@@ -830,7 +903,7 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
             constexpr int MF_RUN = 5, MF_W = 2 * MF_RUN + 19;
             constexpr int c0 = (32 + MF_RUN - 1) / MF_RUN, c1 = c0 + (128 + MF_RUN - 1) / MF_RUN;
             constexpr int cd = (64 + MF_RUN - 1) / MF_RUN;
-            const int n_runs = c1 + cd * a.n_data;
+            const int n_runs = c1 + cd * n_data;
             for (int u = lx; u < n_runs; u += 64) {
                 int s0, e;
                 if (u < c0) {
@@ -845,7 +918,7 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
                 const int n_lo = p + 2 * s0 - 20;                // first sample read
                 if (n_lo >= 0 && p + 2 * (e - 1) < L) {
                     float xr[MF_W], xi[MF_W];                    // x[k] = sample n_lo + k
-                    const int si = im_mod(a, im0 + n_lo);
+                    const int si = im_mod(im0 + n_lo);
                     if (par_r) lds_readn<1>(rbase, off + n_lo, xr); else lds_readn<0>(rbase, off + n_lo, xr);
                     if (par_i) lds_readn<1>(imt, si, xi); else lds_readn<0>(imt, si, xi);
 #pragma unroll
@@ -894,9 +967,10 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
         // 2 pi (fc + ff) Ts k, evaluated in fp64 revolutions (the reference's two double-precision cexp
         // products rounded to float twice; the same rotation to fp32 rounding), the result handed off
         // directly: LTF1 [192,256), LTF2 [256,320), data d [336 + 80 d, +64) (OFDM.c:830-850, 1024-1040) ----
-        const int nw = 2 + a.n_data;
-        float2 *dst = win_item(a.win, a.ipb, nw, i);
-        const int row = a.ipb * nw;                            // float2 between samples n and n + 1
+        const int nw = 2 + n_data;
+        const int ipb = FIX ? (SYM_THREADS / 4) / ((FIX_ND + 1) / 2) : a.ipb;
+        float2 *dst = win_item(a.win, ipb, nw, i);
+        const int row = ipb * nw;                              // float2 between samples n and n + 1
         const double fcf_ts = (fc + ff) * TS;
         // hand-off element j = sample j / nw of window j % nw: consecutive lanes fill the item's nw adjacent
         // slots of a tile row (j / nw by a 16-bit reciprocal, exact for j < 64 nw <= 640); the dump rotates
@@ -912,11 +986,11 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
                     w = (k - 192) >> 6; n = (k - 192) & 63;
                 } else if (k >= 336) {
                     const int d = (k - 336) / 80, o = k - 336 - 80 * d;
-                    if (d < a.n_data && o < 64) { w = 2 + d; n = o; }
+                    if (d < n_data && o < 64) { w = 2 + d; n = o; }
                 }
             }
             const float2 v = cfo_rot(fr[k], fcf_ts, k);
-            if (dbg) a.dbg_frame[k] = v;
+            if (!FIX && dbg) a.dbg_frame[k] = v;
             if (w >= 0) dst[n * row + w] = v;
         }
         FR_STAMP(4);                                           // coarse + fine CFO + hand-off
@@ -925,7 +999,7 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
             if (sync_fail) atomicAdd(&acc[q * ns + 0], 1ull);
             if (oob) atomicAdd(&acc[q * ns + 1], 1ull);
             if (a.pidx_out) a.pidx_out[(int64_t)q * a.n_trials + ti] = p;
-            if (first_item && a.dbg_ints) { a.dbg_ints[0] = p; a.dbg_ints[1] = sync_fail; a.dbg_ints[2] = oob; a.dbg_ints[3] = rx_start; }
+            if (!FIX && first_item && a.dbg_ints) { a.dbg_ints[0] = p; a.dbg_ints[1] = sync_fail; a.dbg_ints[2] = oob; a.dbg_ints[3] = rx_start; }
         }
         // the next item: the next one of this run, or the first of the run fetched at this run's start
         if (i + 1 < run_end) {
@@ -948,7 +1022,7 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
         const unsigned long long *sl = acc + k * ns;
         if (sl[0]) atomicAdd(&c[OFDM_C_SYNC_FAIL], sl[0]);
         if (sl[1]) atomicAdd(&c[OFDM_C_OOB], sl[1]);
-        if (a.word_stats) {
+        if (ns == 4) {          // word_stats
             atomicMin(reinterpret_cast<long long *>(&c[OFDM_C_WL_MIN_Q]), (long long)sl[2]);
             atomicMax(reinterpret_cast<long long *>(&c[OFDM_C_WL_MAX_Q]), (long long)sl[3]);
         }
@@ -959,7 +1033,6 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
 // LS estimate + CP strip + fft + ZF + slicer + demap (OFDM.c:830-1165) for a batch of items: a quad
 // carries {LTF1, LTF2, D_2k, D_2k+1} of one item (estimate formed inside the quad with two DPP
 // broadcasts), ceil(n_data / 2) quads per item, 16 quads per wave.
-constexpr int SYM_THREADS = 256;
 template <bool DUMP>   // DUMP: item 0's bits / subcarriers / metrics for ofdm_receiver
 #ifndef FRAME_SYM_MINB
 #define FRAME_SYM_MINB 2   // 3 waves/SIMD spills 196 VGPRs: frame mode 9 % slower
@@ -1176,6 +1249,12 @@ static unsigned occupancy_grid(const void *kernel, int threads, size_t lds, int 
 #define FRAME_CHUNK_LOG2 22
 #endif
 constexpr int64_t FRAME_CHUNK_ITEMS = int64_t(1) << FRAME_CHUNK_LOG2;
+// items per chunk for n_data data symbols: 2^22, capped so that the hand-off buffer holds no more windows than the
+// reference message's 2^22 items do (8 GiB; ADVICE r3: 8-symbol messages would otherwise take 21 GB)
+static int64_t frame_chunk_items(int n_data) {
+    return std::min<int64_t>(FRAME_CHUNK_ITEMS, FRAME_CHUNK_ITEMS * 4 / (2 + n_data));
+}
+constexpr int64_t FRAME_CHUNK_MIN = int64_t(1) << 16;    // halving stops here when the buffer cannot be allocated
 
 // K4b then K4b' over a.n_items items starting at a.item0, through the context's hand-off buffer
 static int run_frame_chunk(Ctx *c, FrameArgs &a) {
@@ -1196,15 +1275,23 @@ static int run_frame_chunk(Ctx *c, FrameArgs &a) {
 #endif
     const size_t lds = frame_lds_bytes(a.cap_len, a.n_data, a.n_snr, a.imt_len, a.word_stats) + FRAME_LDS_PAD;
     a.fr_in_cap = fr_in_capture(a.cap_len, a.n_data);
+    a.region_floats = wave_region_floats(a.cap_len, a.n_data);
     if (!c->d_work) HIPOK(hipMalloc(&c->d_work, 256));
     a.work = (unsigned long long *)c->d_work;
     HIPOK(hipMemsetAsync(c->d_work, 0, sizeof(unsigned long long), c->stream));
-    // one resident grid: every wave starts with a run of items, the rest come from the work counter
+    // one resident grid: every wave starts with a run of items, the rest come from the work counter.  The
+    // reference message's sweep (2 data symbols, the default 3008-sample capture, no dumps / word-length
+    // statistics) runs the instantiation with that geometry folded in; OFDM_FRAME_GENERIC=1 forces the generic
+    // one (the equivalence test)
     const int64_t runs = (a.n_items + FRAME_ITEM_RUN - 1) / FRAME_ITEM_RUN;
-    hipLaunchKernelGGL(frame_sync_kernel,
-                       dim3(occupancy_grid(reinterpret_cast<const void *>(&frame_sync_kernel), SYNC_THREADS, lds,
-                                           c->cus, (runs + SYNC_WAVES - 1) / SYNC_WAVES, 1)),
-                       dim3(SYNC_THREADS), lds, c->stream, a);
+    const bool fixed = a.n_data == 2 && a.cap_len == cap_len_for(2) && a.wave_len == wave_len_for(2) && !a.ext &&
+                       !a.dbg_res && !a.dbg_ints && !a.dbg_bits && !a.dbg_eq && !a.dbg_corr && !a.dbg_frame &&
+                       !a.word_stats && !getenv("OFDM_FRAME_GENERIC");
+    const void *ks = fixed ? reinterpret_cast<const void *>(&frame_sync_kernel<2, 3008>)
+                           : reinterpret_cast<const void *>(&frame_sync_kernel<0, 0>);
+    const dim3 gs(occupancy_grid(ks, SYNC_THREADS, lds, c->cus, (runs + SYNC_WAVES - 1) / SYNC_WAVES, 1));
+    if (fixed) hipLaunchKernelGGL((frame_sync_kernel<2, 3008>), gs, dim3(SYNC_THREADS), lds, c->stream, a);
+    else hipLaunchKernelGGL((frame_sync_kernel<0, 0>), gs, dim3(SYNC_THREADS), lds, c->stream, a);
     const int ipb = (SYM_THREADS / 4) / ((a.n_data + 1) / 2);
     const bool dump = a.dbg_eq || a.dbg_bits || a.dbg_res;
     const void *k = dump ? reinterpret_cast<const void *>(&frame_sym_kernel<true>)
@@ -1353,11 +1440,19 @@ int ofdm_frame_sweep(ofdm_ctx *ctx, const ofdm_cfg *cfg, const ofdm_rx_opts *opt
 #endif
         const int64_t items = n_trials * a.n_snr;
         c->tic(Ctx::K_FRAME);
-        for (int64_t i0 = 0; i0 < items; i0 += FRAME_CHUNK_ITEMS) {
+        int64_t chunk = frame_chunk_items(a.n_data);
+        for (int64_t i0 = 0; i0 < items;) {
             a.item0 = i0;
-            a.n_items = std::min(FRAME_CHUNK_ITEMS, items - i0);
+            a.n_items = std::min(chunk, items - i0);
             a.add_totals = i0 + a.n_items >= items;
-            if ((rc = run_frame_chunk(c, a))) { c->toc(); return rc; }
+            rc = run_frame_chunk(c, a);
+            if (rc == OFDM_E_NOMEM && chunk > FRAME_CHUNK_MIN) {   // nothing launched yet: a smaller buffer
+                (void)hipGetLastError();
+                chunk /= 2;
+                continue;
+            }
+            if (rc) { c->toc(); return rc; }
+            i0 += a.n_items;
         }
         c->toc();
 #ifdef OFDM_FRAME_STAMPS

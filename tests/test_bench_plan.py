@@ -187,6 +187,23 @@ def test_kernel_build_id_ignores_code_placement(pkg, tmp_path):
         assert (codeobj.workload_build_id(mod, "c3") == codeobj.workload_build_id(lib, "c3")) == same, off
 
 
+def test_kernel_build_id_covers_non_inlined_callees(pkg, monkeypatch):
+    """a device function the compiler did not inline is code the kernel runs.  The id hashes every
+    non-kernel function of the code object that holds the kernel, and nothing of the other code objects."""
+    from ofdm_amd import codeobj
+    FUNC, OBJ = codeobj.STT_FUNC, 1
+
+    def objs(callee: bytes, other: bytes):
+        return [{"k_frame_sync_kernelILi2ELi3008E": (FUNC, b"\x01" * 8), "k_frame_sync_kernelILi2ELi3008E.kd":
+                 (OBJ, bytes(64)), "helper_fn": (FUNC, callee), "__hip_cuid_x": (OBJ, b"\x00")},
+                {"rx_pack_kernelILi2ELi0ELi0ELb0E": (FUNC, b"\x02" * 8), "other_fn": (FUNC, other)}]
+    ids = {}
+    for key, args in (("a", (b"\xaa", b"\x00")), ("callee", (b"\xab", b"\x00")), ("other", (b"\xaa", b"\x01"))):
+        monkeypatch.setattr(codeobj, "_code_objects", lambda p, m, _a=args: objs(*_a))
+        ids[key] = codeobj.kernel_build_id(__file__, ("frame_sync_kernelILi2ELi3008E",))
+    assert ids["a"] != ids["callee"] and ids["a"] == ids["other"]
+
+
 def test_host_cpu_share_is_derived(monkeypatch):
     b = _bench()
     monkeypatch.setattr(b, "_cgroup_cpu_quota", lambda: (3.0, "cgroup v2 cpu.max 300000/100000"))
@@ -268,6 +285,23 @@ def test_pending_next_tx_survives_a_failed_rx_and_is_built_by_symbol_sweep(engin
     tx, bits = fresh()
     engine.set_next_tx(cfg, 4096, 300, tx, bits)
     engine.symbol_sweep(cfg, [5.0], 1000)                # flushes the pending batch first
+    assert same(tx, bits)
+
+    # a pending batch that shares bytes with the call's own batch is refused (it would be written
+    # while read, or by two groups of one launch), and stays pending
+    tx, bits = fresh()
+    engine.set_next_tx(cfg, 4096, 300, tx, bits)
+    sub_bits = bits[64:]                                  # overlaps the pending batch's bit rows
+    rc = engine.lib.ofdm_txrx_frames(engine.ctx, C.byref(cfg), 0, 20, C.c_void_p(tx0.data_ptr()),
+                                     C.c_void_p(sub_bits.data_ptr()), snr.ctypes.data_as(C.c_void_p), 2,
+                                     C.c_void_p(cnt.data_ptr()))
+    assert rc == -1 and b"overlaps" in engine.lib.ofdm_last_error()
+    rc = engine.lib.ofdm_rx_frames(engine.ctx, C.byref(cfg), C.c_void_p(tx.data_ptr()), C.c_void_p(bits0.data_ptr()),
+                                   0, 256, snr.ctypes.data_as(C.c_void_p), 2, C.c_void_p(cnt.data_ptr()))
+    assert rc == -1                                      # reading the batch that is to be built
+    torch.cuda.synchronize()
+    assert np.all(bits.cpu().numpy() == -1)
+    engine.rx_frames(cfg, tx0, bits0, 0, 256, snr, cnt)
     assert same(tx, bits)
 
 

@@ -132,6 +132,24 @@ def test_lazy_capture_equals_full_evaluation(engine, pkg, monkeypatch):
     assert np.array_equal(lazy8, full8)
 
 
+@pytest.mark.parametrize("no_lazy", [False, True])
+def test_fixed_geometry_kernel_equals_generic(engine, pkg, monkeypatch, no_lazy):
+    """The reference message's sweep (2 data symbols, the 3008-sample capture of OFDM.c:945) runs the sync
+    kernel instantiated with that geometry as compile-time constants; OFDM_FRAME_GENERIC=1 runs the generic
+    instantiation (every size from the arguments, as for other messages and the parity dumps).  Every counter
+    and packet_idx is identical, lazy or full evaluation, over the bench's SNR grid."""
+    snrs = np.arange(0.0, 31.0, 2.0)
+    cfg = pkg.make_cfg(payload="message")
+    if no_lazy:
+        monkeypatch.setenv("OFDM_FRAME_NO_LAZY", "1")
+    fixed, fp = engine.frame_sweep(cfg, snrs, 4000, want_packet_idx=True, first_trial=77)
+    monkeypatch.setenv("OFDM_FRAME_GENERIC", "1")
+    gen, gp = engine.frame_sweep(cfg, snrs, 4000, want_packet_idx=True, first_trial=77)
+    assert np.array_equal(fp, gp)
+    assert np.array_equal(fixed, gen)
+    assert fixed[0, 0] == 4000
+
+
 def test_frame_sweep_two_chunks_equal_their_halves(engine, pkg):
     """A sweep of more than 2^22 (trial, SNR) items runs as several sync -> symbol launch pairs through the
     hand-off buffer: its counters and packet_idx equal those of two sweeps of half the trials each (one
