@@ -12,9 +12,9 @@ Workloads (BASELINE.json configs; --workload):
      GPU (weak scaling: the largest single-GPU config; the driver's 1/2/4/8-GPU curve runs this)
   c2 (configs[1])          ideal CSI, 1e6 symbols/point, 1 GPU
   c4 (configs[3])          c3's chain, 1e8 symbols/point in TOTAL, split over the ranks (strong)
-  c5 (configs[4])          4-tap Rayleigh + ZF (LS), real AWGN (every config uses the
-                           reference's real-only noise), 1e9 symbol-SNR evaluations in TOTAL (6.25e7
-                           symbols/point x 16 points), split over the ranks (strong)
+  c5 (configs[4])          1e9 symbol-SNR evaluations in TOTAL (6.25e7 symbols/point x 16 points; not 1e9
+                           symbols per point), split over the ranks (strong): 4-tap Rayleigh + ZF (LS), real
+                           AWGN (every config uses the reference's real-only noise)
   frame                    the reference's own trial (sync, CFO, LS): the like-for-like line next
                            to the reference's trial loop on the host
 
@@ -57,8 +57,8 @@ WORKLOADS = {
            dict(est="ideal", noise="real", channel="awgn", conv="c", payload="random"), 1_000_000, "weak"),
     "c4": ("BASELINE configs[3]: c3's chain, 1e8 symbols/point in total, counter-range shards over the ranks, "
            "RCCL all-reduce of the int64 counters", _LS_AWGN, 100_000_000, "strong"),
-    "c5": ("BASELINE configs[4]: 4-tap Rayleigh + per-subcarrier ZF (LTF LS), real AWGN, full BER/EVM sweep, "
-           "1e9 symbol-SNR evaluations in total (6.25e7 symbols/point x 16) over the ranks",
+    "c5": ("1e9 symbol-SNR evaluations in total (6.25e7 symbols/point x 16 SNR points, split over the ranks) -- "
+           "BASELINE configs[4]: 4-tap Rayleigh + per-subcarrier ZF (LTF LS), real AWGN, full BER/EVM sweep",
            dict(est="ls", noise="real", channel="rayleigh4", conv="c", payload="random"),
            62_500_000, "strong"),
     "frame": ("frame mode: OFDM.c Transmission_Over_Air + Receiver trials (sync, CFO, LS), reference message; the "

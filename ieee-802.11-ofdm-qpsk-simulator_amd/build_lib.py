@@ -40,7 +40,7 @@ SOURCE_FLAGS = {"ofdm_symbol.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
 
 # Kernels whose parity-dump variants (last template argument `true`) are allowed to spill: they
 # write every equalised bin and run only in tests.  Every other kernel must build spill-free.
-DUMP_KERNEL = re.compile(r"^ofdm::(rx_\w+|frame_sym)_kernel<.*true>$")
+DUMP_KERNEL = re.compile(r"^ofdm::(rx_\w+_kernel<.*true>|frame_sym_kernel<true, \d+>)$")
 RESOURCE_REPORT = BUILD / "resource_usage.json"
 
 

@@ -212,6 +212,30 @@ __device__ __forceinline__ float wave_sum_f(float v) {
            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)) +
            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
 }
+// atan2f for the CFO estimates (OFDM.c:798, 821): the device library's atan2f (OCML) without its frexp / ldexp
+// scaling of the quotient and its inf / NaN cases.  For finite normal arguments min(|x|,|y|) * rcp(max) is the
+// library's scaled quotient bit for bit (rcp of a power-of-two-scaled mantissa scales exactly), followed by the
+// same minimax polynomial and quadrant fix-ups, so the result is the library's; (0, 0) gives +-0 as atan2f
+// does for x = +0.
+__device__ __forceinline__ float atan2_cfo(float y, float x) {
+    const float ax = fabsf(x), ay = fabsf(y);
+    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+    float a = mn * __builtin_amdgcn_rcpf(mx);
+    a = mx > 0.f ? a : 0.f;
+    const float s = a * a;
+    float t = fmaf(s, __uint_as_float(0x3b2d2a58u), __uint_as_float(0xbc7a590cu));
+    t = fmaf(s, t, __uint_as_float(0x3d29fb3fu));
+    t = fmaf(s, t, __uint_as_float(0xbd97d4d7u));
+    t = fmaf(s, t, __uint_as_float(0x3dd931b2u));
+    t = fmaf(s, t, __uint_as_float(0xbe1160e6u));
+    t = fmaf(s, t, __uint_as_float(0x3e4cb8bfu));
+    t = fmaf(s, t, __uint_as_float(0xbeaaaa62u));
+    float r = fmaf(a, s * t, a);                                   // atan(a), a in [0, 1]
+    r = ay > ax ? __uint_as_float(0x3fc90fdbu) - r : r;           // pi / 2 - atan(1 / a)
+    r = x < 0.f ? __uint_as_float(0x40490fdbu) - r : r;           // pi - ...
+    return copysignf(r, y);
+}
+
 // wave-uniform max / min of an int: DPP within each row of 16 lanes (quad xor 1, xor 2, half-row and
 // row mirrors), then the four row results by readlane -- no LDS round trips (a __shfl_xor ladder is six
 // serial ds_bpermute)
@@ -293,13 +317,21 @@ __device__ __forceinline__ float2 cfo_rot(float2 v, double f_ts, int i) {
     return make_float2(v.x * c - v.y * s, v.x * s + v.y * c);
 }
 
-// Hand-off layout: tiles of ipb items (one frame_sym_kernel block), each tile [64 samples][ipb items][nw
-// windows] float2, so that a symbol-kernel wave reading sample n of its lanes' windows reads one
-// contiguous row segment (its 16 items x 4 windows = 512 B for the reference frame), where an item-major
-// layout made every lane's 8-byte load a different cache line.
+// Hand-off layout: tiles of ipb items (one frame_sym_kernel block).  Within a tile, samples go in groups of
+// WIN_SG: [64 / WIN_SG groups][ipb items][WIN_SG samples][nw windows] float2, so that
+//   * one item's WIN_SG x nw windows (128 B for the reference frame) are contiguous: the sync wave that owns the
+//     item writes whole 128-B lines (the earlier [64 samples][ipb items][nw] tile wrote 32-B fragments 2 KB apart,
+//     2.03x write amplification);
+//   * a symbol-kernel wave reading sample n of its lanes' windows (16 items x 4 windows for the reference frame)
+//     touches 16 lines that its reads of the group's other WIN_SG - 1 samples hit again in L1.
+constexpr int WIN_SG = 4;
 __host__ __device__ inline float2 *win_item(float2 *win, int ipb, int nw, int64_t item) {
     const int64_t tile = item / ipb, it = item - tile * ipb;
-    return win + tile * 64 * (int64_t)(ipb * nw) + it * nw;      // sample n of window w at [n * ipb * nw + w]
+    return win + tile * 64 * (int64_t)(ipb * nw) + it * (WIN_SG * nw);
+}
+// offset of sample n of window 0 from win_item()
+__host__ __device__ inline int win_off(int n, int ipb, int nw) {
+    return (n / WIN_SG) * (ipb * WIN_SG * nw) + (n % WIN_SG) * nw;
 }
 
 // j-th frame sample the receiver reads (j < 160 + 64 nd): the coarse-CFO lag window [80, 112)
@@ -673,7 +705,11 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
                 // immediate offset (< 1 KB) -- otherwise the compiler folds part of the table base into constants
                 // too large for the offset field and spends one v_add per read on addresses
                 using LdsF = const __attribute__((address_space(3))) float;
+#ifndef FRAME_EXP_NOWRAP
                 LdsF *ti_ = (LdsF *)(imt + im_mod(im0 + n0));
+#else           // A/B timing only (wrong imaginary parts): table reads without the period wrap's bank shift
+                LdsF *ti_ = (LdsF *)(imt + ((im0 + n0) & 1023));
+#endif
                 LdsF *tr_ = (LdsF *)(r + n0);
                 opaque(ti_);
                 opaque(tr_);
@@ -946,22 +982,22 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
         // (OFDM.c:806-828): 64-lag over the two long training symbols after the coarse rotation, the 128
         // rotated LTF samples formed on the fly (the same arithmetic as rotating the whole frame first).
         // Both estimates are wave reductions. ----
+        // every fr[] sample the estimates read, loaded in one LDS round trip (lanes >= 16 read the coarse window
+        // too, and drop it)
+        const float2 cu = fr[80 + (lx & 15)], cw = fr[96 + (lx & 15)], l1 = fr[192 + lx], l2 = fr[256 + lx];
         float2 pp = make_float2(0.f, 0.f);
-        if (lx < 16) {
-            const float2 u = fr[80 + lx], w = fr[96 + lx];
-            pp = make_float2(u.x * w.x + u.y * w.y, u.y * w.x - u.x * w.y);
-        }
+        if (lx < 16) pp = make_float2(cu.x * cw.x + cu.y * cw.y, cu.y * cw.x - cu.x * cw.y);
         pp.x = wave_sum_f(pp.x);
         pp.y = wave_sum_f(pp.y);
-        double fc = (-1.0 / (2.0 * M_PI * 16.0 * TS)) * (double)atan2f(pp.y, pp.x);
+        double fc = (-1.0 / (2.0 * M_PI * 16.0 * TS)) * (double)atan2_cfo(pp.y, pp.x);
         if (a.float_cfo) fc = (double)(float)fc;
         {
-            const float2 u = cfo_rot(fr[192 + lx], fc * TS, 192 + lx), w = cfo_rot(fr[256 + lx], fc * TS, 256 + lx);
+            const float2 u = cfo_rot(l1, fc * TS, 192 + lx), w = cfo_rot(l2, fc * TS, 256 + lx);
             pp = make_float2(u.x * w.x + u.y * w.y, u.y * w.x - u.x * w.y);
         }
         pp.x = wave_sum_f(pp.x);
         pp.y = wave_sum_f(pp.y);
-        double ff = (-1.0 / (2.0 * M_PI * 64.0 * TS)) * (double)atan2f(pp.y, pp.x);
+        double ff = (-1.0 / (2.0 * M_PI * 64.0 * TS)) * (double)atan2_cfo(pp.y, pp.x);
         if (a.float_cfo) ff = (double)(float)ff;
         // ---- coarse then fine rotation (OFDM.c:802, 825) as ONE rotation by the summed phase
         // 2 pi (fc + ff) Ts k, evaluated in fp64 revolutions (the reference's two double-precision cexp
@@ -970,13 +1006,25 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
         const int nw = 2 + n_data;
         const int ipb = FIX ? (SYM_THREADS / 4) / ((FIX_ND + 1) / 2) : a.ipb;
         float2 *dst = win_item(a.win, ipb, nw, i);
-        const int row = ipb * nw;                              // float2 between samples n and n + 1
         const double fcf_ts = (fc + ff) * TS;
-        // hand-off element j = sample j / nw of window j % nw: consecutive lanes fill the item's nw adjacent
-        // slots of a tile row (j / nw by a 16-bit reciprocal, exact for j < 64 nw <= 640); the dump rotates
-        // all nfr samples
+        // hand-off element j = sample j / nw of window j % nw: consecutive lanes fill the item's contiguous
+        // WIN_SG x nw slots of a sample group, 16 lanes one 128-B line for the reference frame (j / nw by a 16-bit
+        // reciprocal, exact for j < 64 nw <= 640); the dump rotates all nfr samples
         const int nrot = dbg ? nfr : 64 * nw;
         const uint32_t inv_nw = (65536u + (uint32_t)nw - 1u) / (uint32_t)nw;
+        if constexpr (FIX && 2 + FIX_ND == 4) {
+            // four windows: lane lx always fills window w = lx & 3 (frame sample kb + n), samples n = 16 t + lx / 4;
+            // the four fr[] reads issued together, then rotated and stored (16 lanes = one 128-B line)
+            const int w = lx & 3, kb = w < 2 ? 192 + 64 * w : 176 + 80 * w;     // 192, 256, 336, 416
+            float2 hv[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) hv[t] = fr[kb + 16 * t + (lx >> 2)];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int n = 16 * t + (lx >> 2);
+                dst[win_off(n, ipb, nw) + w] = cfo_rot(hv[t], fcf_ts, kb + n);
+            }
+        } else
         for (int j = lx; j < nrot; j += 64) {
             int n = (int)(((uint32_t)j * inv_nw) >> 16), w = j - n * nw;
             int k = needed_k(64 * w + n + 32);
@@ -991,7 +1039,7 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
             }
             const float2 v = cfo_rot(fr[k], fcf_ts, k);
             if (!FIX && dbg) a.dbg_frame[k] = v;
-            if (w >= 0) dst[n * row + w] = v;
+            if (w >= 0) dst[win_off(n, ipb, nw) + w] = v;
         }
         FR_STAMP(4);                                           // coarse + fine CFO + hand-off
         if (lx == 0) {
@@ -1033,29 +1081,30 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
 // LS estimate + CP strip + fft + ZF + slicer + demap (OFDM.c:830-1165) for a batch of items: a quad
 // carries {LTF1, LTF2, D_2k, D_2k+1} of one item (estimate formed inside the quad with two DPP
 // broadcasts), ceil(n_data / 2) quads per item, 16 quads per wave.
-template <bool DUMP>   // DUMP: item 0's bits / subcarriers / metrics for ofdm_receiver
+template <bool DUMP, int FIX_ND>   // DUMP: item 0's bits / subcarriers / metrics for ofdm_receiver
 #ifndef FRAME_SYM_MINB
 #define FRAME_SYM_MINB 2   // 3 waves/SIMD spills 196 VGPRs: frame mode 9 % slower
 #endif
+// FIX_ND > 0: n_data as a compile-time constant (the reference message's sweep: the hand-off offsets fold)
 __global__ __launch_bounds__(SYM_THREADS, FRAME_SYM_MINB) void frame_sym_kernel(FrameArgs a) {
+    const int n_data = FIX_ND ? FIX_ND : a.n_data;
     __shared__ unsigned long long acc[OFDM_MAX_SNR][8];
     __shared__ float part_e[SYM_THREADS / 4][2];             // per quad: EVM of its two data symbols
     __shared__ uint32_t part_b[SYM_THREADS / 4][2], part_a[SYM_THREADS / 4][2];
     for (int k = threadIdx.x; k < a.n_snr * 8; k += SYM_THREADS) (&acc[0][0])[k] = 0ull;
     __syncthreads();
     const int lane = threadIdx.x & 63, quad = threadIdx.x >> 2, role = lane & 3;
-    const int qpi = (a.n_data + 1) / 2, ipb = (SYM_THREADS / 4) / qpi;   // quads per item, items per block
+    const int qpi = (n_data + 1) / 2, ipb = (SYM_THREADS / 4) / qpi;   // quads per item, items per block
     const int item_l = quad / qpi, qi = quad - item_l * qpi;
     const int dsym = 2 * qi + (role & 1);
-    const int nw = 2 + a.n_data;
-    const int dsc = min(dsym, a.n_data - 1);
+    const int nw = 2 + n_data;
+    const int dsc = min(dsym, n_data - 1);
     const int w = role < 2 ? role : 2 + dsc;
     for (int64_t base = (int64_t)blockIdx.x * ipb; base < a.n_items; base += (int64_t)gridDim.x * ipb) {
         const int64_t i = base + item_l;
         const bool item_ok = item_l < ipb && i < a.n_items;
-        const bool dlane = item_ok && role >= 2 && dsym < a.n_data;
+        const bool dlane = item_ok && role >= 2 && dsym < n_data;
         const float2 *src = win_item(a.win, ipb, nw, item_ok ? i : base) + w;
-        const int row = ipb * nw;                                  // float2 between samples n and n + 1
         float2 x[64];
         // load fused with the first radix-4 stage, 16 samples at a time (fft() = DFT(x (-1)^n))
         static_for<0, 4>([&](auto gc) {
@@ -1064,7 +1113,7 @@ __global__ __launch_bounds__(SYM_THREADS, FRAME_SYM_MINB) void frame_sym_kernel(
             opaque(sp);
             static_for<0, 16>([&](auto pc) {
                 constexpr int n = 16 * (decltype(pc)::value >> 2) + 4 * g + (decltype(pc)::value & 3);
-                const float2 v = gld(sp, n * row);
+                const float2 v = gld(sp, win_off(n, ipb, nw));
                 x[n] = (n & 1) ? make_float2(-v.x, -v.y) : v;
             });
             static_for<0, 4>([&](auto ic) { dif_stage1<false, 4 * g + decltype(ic)::value>(x); });
@@ -1103,7 +1152,7 @@ __global__ __launch_bounds__(SYM_THREADS, FRAME_SYM_MINB) void frame_sym_kernel(
             atomicAdd(&sl[0], (unsigned long long)ferr);
             atomicAdd(&sl[1], (unsigned long long)(ferr > 0u));
             atomicAdd(&sl[2], (unsigned long long)fax);
-            const float N = 48.0f * (float)a.n_data;
+            const float N = 48.0f * (float)n_data;
             atomicAdd(&sl[5], (unsigned long long)(int64_t)__float2ll_rn(fe * (float)OFDM_EVM_Q_SCALE));
             const float db = fe > 0.f ? fmaxf(3.01029995663981195214f * __builtin_amdgcn_logf(fe / N), -400.f) : -400.f;
             atomicAdd(&sl[6], (unsigned long long)(int64_t)__float2ll_rn(db * (float)OFDM_EVM_Q_SCALE));
@@ -1113,7 +1162,7 @@ __global__ __launch_bounds__(SYM_THREADS, FRAME_SYM_MINB) void frame_sym_kernel(
                 atomicAdd(&sl[7], (unsigned long long)(int64_t)__float2ll_rn(dbp * (float)OFDM_EVM_Q_SCALE));
                 atomicAdd(&sl[4], 1ull);
             }
-            if (DUMP && g == 0 && a.dbg_res) { a.dbg_res[0] = db; a.dbg_res[1] = dbp; a.dbg_res[2] = (float)ferr / (96.0f * a.n_data); }
+            if (DUMP && g == 0 && a.dbg_res) { a.dbg_res[0] = db; a.dbg_res[1] = dbp; a.dbg_res[2] = (float)ferr / (96.0f * n_data); }
         }
         __syncthreads();
     }
@@ -1294,11 +1343,14 @@ static int run_frame_chunk(Ctx *c, FrameArgs &a) {
     else hipLaunchKernelGGL((frame_sync_kernel<0, 0>), gs, dim3(SYNC_THREADS), lds, c->stream, a);
     const int ipb = (SYM_THREADS / 4) / ((a.n_data + 1) / 2);
     const bool dump = a.dbg_eq || a.dbg_bits || a.dbg_res;
-    const void *k = dump ? reinterpret_cast<const void *>(&frame_sym_kernel<true>)
-                         : reinterpret_cast<const void *>(&frame_sym_kernel<false>);
+    const bool sym2 = a.n_data == 2 && !getenv("OFDM_FRAME_GENERIC");     // the hand-off offsets folded
+    const void *k = dump ? reinterpret_cast<const void *>(&frame_sym_kernel<true, 0>)
+                  : sym2 ? reinterpret_cast<const void *>(&frame_sym_kernel<false, 2>)
+                         : reinterpret_cast<const void *>(&frame_sym_kernel<false, 0>);
     const dim3 grid(occupancy_grid(k, SYM_THREADS, 0, c->cus, (a.n_items + ipb - 1) / ipb));
-    if (dump) hipLaunchKernelGGL(frame_sym_kernel<true>, grid, dim3(SYM_THREADS), 0, c->stream, a);
-    else hipLaunchKernelGGL(frame_sym_kernel<false>, grid, dim3(SYM_THREADS), 0, c->stream, a);
+    if (dump) hipLaunchKernelGGL((frame_sym_kernel<true, 0>), grid, dim3(SYM_THREADS), 0, c->stream, a);
+    else if (sym2) hipLaunchKernelGGL((frame_sym_kernel<false, 2>), grid, dim3(SYM_THREADS), 0, c->stream, a);
+    else hipLaunchKernelGGL((frame_sym_kernel<false, 0>), grid, dim3(SYM_THREADS), 0, c->stream, a);
     HIPOK(hipGetLastError());
     return OFDM_OK;
 }

@@ -210,6 +210,17 @@ static __device__ unsigned long long g_pack_stamps[4][8];
 #ifndef OFDM_RX_PACK_FADE_WAVES     // the Rayleigh LS receiver (72 KB of LDS: two blocks per CU)
 #define OFDM_RX_PACK_FADE_WAVES 2
 #endif
+#ifndef PACK_SACC_SUB_LS
+#define PACK_SACC_SUB_LS 4  // copies of the block's SNR accumulators, LS receivers (see sacc; at most 4 for the
+                            // Rayleigh one, whose two blocks per CU leave room for no more).  A/B (round 4,
+                            // profiles/r04/ab): c3 1.236 -> 1.260e10, c5 1.193 -> 1.220e10; 8 copies the same
+#endif
+#ifndef OFDM_PACK_SPEC_LIN
+#define OFDM_PACK_SPEC_LIN 1    // the prologue's clean-spectrum stores: a wave's lanes on consecutive frames (A/B)
+#endif
+#ifndef PACK_SACC_SUB
+#define PACK_SACC_SUB 1     // the same for the ideal-CSI receiver (2 copies spill it at its 168-VGPR budget)
+#endif
 template <int KIND, int CONV, int CHAN, bool DUMP>
 __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFDM_RX_PACK_FADE_WAVES : OFDM_RX_PACK_WAVES)
                                             : OFDM_RX_PACK_IDEAL_WAVES) void rx_pack_kernel(RxArgs a) {
@@ -222,7 +233,11 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
     constexpr bool EEL = KIND == 2 && EE_LDS_N > 0;
     static_assert(!(SPLIT && EEL), "the split loop keeps the whole E spectrum in VGPRs");
 #ifndef OFDM_NO_PACK_WARM_LATE
-    constexpr bool WLATE = KIND == 2 && !FADE;      // where the next item's L2 warm-up is issued (see the SNR loop)
+#ifndef OFDM_PACK_WLATE_FADE
+#define OFDM_PACK_WLATE_FADE 0      // A/B option: the late warm-up in the Rayleigh LS receiver too
+#endif
+    // where the next item's L2 warm-up is issued (see the SNR loop)
+    constexpr bool WLATE = KIND == 2 && (!FADE || OFDM_PACK_WLATE_FADE);
 #else
     constexpr bool WLATE = false;
 #endif
@@ -230,7 +245,17 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
     __shared__ __attribute__((aligned(16))) float4 ce[PACK_PAIRS];                   // LS: FFT((-1)^n 2T[n])
     __shared__ __attribute__((aligned(16))) float4 fce[FADE ? PACK_PAIRS : 1][FADE ? PK_FRAMES : 1];  // 24 KB: H' FFT(2T)
     __shared__ __attribute__((aligned(8))) uint32_t truth[3][PK_SYMS];               // pair-order words
-    __shared__ unsigned long long sacc[OFDM_MAX_SNR][5];         // flush_lanes' five slots per SNR point
+    // flush_lanes' five slots per SNR point; for the first SACC_XQ points SUBN - 1 more copies: lane l adds into
+    // copy l % SUBN, so that an SNR iteration's 5 x 64 same-address LDS atomics (the kernel's LDS bank-conflict
+    // cycles) spread over SUBN addresses in distinct banks; the copies are summed before the flush
+    constexpr int SUBN = KIND != 2 ? PACK_SACC_SUB : FADE ? (PACK_SACC_SUB_LS < 4 ? PACK_SACC_SUB_LS : 4) : PACK_SACC_SUB_LS;
+    constexpr int SACC_XQ = 16;
+    __shared__ unsigned long long sacc[OFDM_MAX_SNR][5];
+    __shared__ unsigned long long sacx[SUBN > 1 ? SACC_XQ : 1][SUBN > 1 ? 5 * (SUBN - 1) : 1];
+    auto slots = [&](int q, int ln) -> unsigned long long * {
+        const int c = ln % SUBN;
+        return SUBN > 1 && c > 0 && q < SACC_XQ ? &sacx[q][5 * (c - 1)] : sacc[q];
+    };
     __shared__ uint32_t pf_dummy[64];                             // L2 warm-up destination (never read)
     __shared__ __attribute__((aligned(8))) float2 eel[EEL ? 4 : 1][EEL ? EE_LDS_N : 1][EEL ? 64 : 1];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -240,6 +265,8 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
     unsigned long long st_t = __builtin_amdgcn_s_memtime();
 #endif
     for (int i = tid; i < a.n_snr * 5; i += blockDim.x) (&sacc[0][0])[i] = 0ull;
+    if constexpr (SUBN > 1)
+        for (int i = tid; i < SACC_XQ * 5 * (SUBN - 1); i += blockDim.x) (&sacx[0][0])[i] = 0ull;
     if constexpr (KIND == 2) {
         // the E window's clean samples 2T[n] (both LTF slots hold T): one spectrum per block
         if (wv == 0) {
@@ -321,7 +348,14 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
 #else
         if (t < PK_SYMS) {
 #endif
+#if OFDM_PACK_SPEC_LIN
+            // thread t: symbol 2 f + d of the group with d = t / 64, f = t % 64, so that a wave's 64 lanes store
+            // 64 consecutive frames' pairs (conflict-free ds_write_b128; with symbol t per thread, lanes t and
+            // t + 1 stored to the two halves, 1 KB apart, on the same banks: 2-way conflicts on every store)
+            clean_spectrum<SPLIT>(a, grp * PK_SYMS + 2 * (t & 63) + (t >> 6), &spec[0][t >> 6][t & 63]);
+#else
             clean_spectrum<SPLIT>(a, grp * PK_SYMS + t, &spec[0][t & 1][t >> 1]);
+#endif
         } else {
             const int j = t - PK_SYMS;
             const uint32_t *src = a.bits + 7 * a.pitch + grp * PK_SYMS + j;
@@ -580,7 +614,7 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
                 });
                 FrameAcc acc;
                 frame_metrics(acc, 4.0f * evm, be, ax);
-                flush_lanes(acc, valid, sacc[q]);
+                flush_lanes(acc, valid, slots(q, lane));
             } else {
             // ---- data windows: x[n] = (-1)^n (d0[n] + j d1[n]) fused with the first radix-4 stage.
             // Gaussian t of the frame's stream is sample t of the frame timeline: D0 at
@@ -741,10 +775,21 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
             }
             FrameAcc acc;
             frame_metrics(acc, KIND == 2 ? 4.0f * evm : evm, be, ax);
-            flush_lanes(acc, valid, sacc[q]);
+            flush_lanes(acc, valid, slots(q, SPLIT ? lane_fresh() : lane));
             }   // !SPLIT
         }
         PK_STAMP(4);                                     // SNR loop
+    }
+    if constexpr (SUBN > 1) {       // fold the copies into sacc
+        __syncthreads();
+        const int ft = SPLIT ? (wv << 6) + lane_fresh() : tid;
+        for (int i = ft; i < min(a.n_snr, SACC_XQ) * 5; i += 256) {
+            const int q = i / 5, k = i % 5;
+            unsigned long long v = sacc[q][k];
+#pragma unroll
+            for (int c = 1; c < SUBN; ++c) v += sacx[q][5 * (c - 1) + k];
+            sacc[q][k] = v;
+        }
     }
     block_flush(a, sacc, SPLIT ? (wv << 6) + lane_fresh() : tid);
     PK_STAMP(5);                                           // block flush

@@ -175,7 +175,7 @@ def _drop_trials(sweep, snrs, trials, n_counters=16):
 def test_frame_sweep_evm_counters_vs_oracle(engine, oracle, pkg):
     """The counters behind Output_EVM_AGC.txt / Output_EVM_AGC_DB.txt (OFDM.c:1104-1150, 1228-1231):
     EVM_PRE_Q (7), EVM_POST_AXIS (8), EVMDB_PRE_Q (9), EVMDB_POST_Q (10), EVMDB_POST_FINITE (11) of
-    the batched sweep (frame_sym_kernel<false>) vs the oracle on the same Philox streams.  Trials
+    the batched sweep (frame_sym_kernel<false, 2>) vs the oracle on the same Philox streams.  Trials
     whose packet_idx differs (fp32 vs double at the 0.75 threshold) are re-run one by one on both
     sides and subtracted, so the remaining trials are compared tightly."""
     snrs = [0.0, 3.0, 6.0, 8.0, 10.0, 14.0, 30.0]
