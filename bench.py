@@ -65,7 +65,13 @@ WORKLOADS = {
               "capture's tail is generated only when the first detection round does not decide Packet_Selection "
               "(results bit-identical to full evaluation, OFDM_FRAME_NO_LAZY)",
               dict(payload="message", noise="real", conv="c"), 1_000_000, "weak"),
+    "frame8": ("frame mode with a 96-character message (8 data symbols per frame, 5955-sample captures: the long-"
+               "message path); units are data symbols x SNR points",
+               dict(payload="message", noise="real", conv="c"), 1_000_000, "weak"),
 }
+# data symbols per frame (trial) of each workload; frame8 sets its message before the sweep
+FRAME_DATA = {"frame8": 8}
+FRAME8_MESSAGE = (b"The quick brown fox jumps over the lazy dog; 802.11a OFDM-QPSK frames on MI355X, eight symbols.. ")[:96]
 
 
 def load_pmc(workload: str) -> dict:
@@ -243,7 +249,7 @@ def cpu_baseline(workload: str, seconds: float = 12.0, share: dict | None = None
     except Exception as e:  # pragma: no cover
         return {"value": None, "unit": "OFDM symbols/s", "cores": 0, "kind": "reference",
                 "sample": f"unavailable: {e}"}
-    frame = workload == "frame"
+    frame = workload.startswith("frame")     # frame8: the reference has only its own 2-symbol message
     rayleigh = workload == "c5"
     ideal = workload == "c2"
     if frame:
@@ -386,7 +392,8 @@ def main():
     desc, kw, symbols, scaling = WORKLOADS[args.workload]
     if args.symbols:
         symbols = args.symbols
-    total_frames = symbols // 2                  # D = 2 data symbols per frame
+    dpf = FRAME_DATA.get(args.workload, 2)         # D data symbols per frame (2: OFDM.c:439)
+    total_frames = symbols // dpf
     if scaling == "weak":
         first, end = odist.weak_range(total_frames, rank)
     else:
@@ -394,7 +401,9 @@ def main():
     frames = end - first
     cfg = pkg.make_cfg(**kw)
     eng = pkg.Engine(dev)
-    frame_mode = args.workload == "frame"
+    frame_mode = args.workload.startswith("frame")
+    if args.workload == "frame8":
+        assert eng.set_message(FRAME8_MESSAGE) == 8
     counters = eng.new_counters(len(SNR_GRID))
     chunks = plan_chunks(first, frames, args.chunks)
     # real-noise sweeps on the packed receivers (c2, c3, c4, c5): every Tx batch built inside the receivers
@@ -404,7 +413,7 @@ def main():
                 if not frame_mode and chunks else None)
 
     def step():
-        if frame_mode:            # one trial = one frame of 2 data symbols; waveform cached on the device
+        if frame_mode:            # one trial = one frame of dpf data symbols; waveform cached on the device
             c = eng.frame_sweep(cfg, SNR_GRID, frames, first_trial=first)
             counters.copy_(torch.from_numpy(c))
         elif sym_step is not None:
@@ -440,10 +449,10 @@ def main():
     c = counters.cpu().numpy()
     n_snr = len(SNR_GRID)
     job_frames = total_frames * (world if scaling == "weak" else 1)
-    total_units = float(job_frames) * 2 * n_snr * args.steps          # symbol-SNR evaluations, all ranks
+    total_units = float(job_frames) * dpf * n_snr * args.steps        # symbol-SNR evaluations, all ranks
     value = total_units / elapsed
     rx_avg_s = rx_ms / max(rx_n, 1) / 1e3
-    units_per_launch = frames * 2 * n_snr * args.steps / max(rx_n, 1)  # this rank's units per receiver launch
+    units_per_launch = frames * dpf * n_snr * args.steps / max(rx_n, 1)  # this rank's units per receiver launch
     bytes_per_unit = FRAME_CAPTURE_BYTES / 2 if frame_mode else BYTES_PER_SYMBOL_SNR
     res = pkg.SweepResult(SNR_GRID, c)
     pmc = load_pmc(args.workload)
@@ -473,8 +482,8 @@ def main():
             "data": "synthetic (Philox4x32-10 bits and noise, seed 0x80211A)",
             "config": {"workload": args.workload, "description": desc,
                        "symbols_per_snr": symbols if scaling == "strong" else symbols * world,
-                       "symbols_per_snr_per_gpu": 2 * frames, "snr_db": SNR_GRID.tolist(),
-                       "frames_per_gpu": frames, "data_symbols_per_frame": 2, "chunks_per_step": len(chunks),
+                       "symbols_per_snr_per_gpu": dpf * frames, "snr_db": SNR_GRID.tolist(),
+                       "frames_per_gpu": frames, "data_symbols_per_frame": dpf, "chunks_per_step": len(chunks),
                        "parallelism": (f"dp{world} (counter-range shards, {scaling} scaling; 1 RCCL all-reduce of "
                                        "int64 counters per step)" if distributed
                                        else "1 process, no collective (not launched under torchrun)")},

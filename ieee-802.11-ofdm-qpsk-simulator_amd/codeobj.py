@@ -29,6 +29,7 @@ WORKLOAD_KERNELS = {
     "c5": ("rx_pack_kernelILi2ELi0ELi1ELb0E",),
     "c2": ("rx_pack_kernelILi0ELi0ELi0ELb0E",),
     "frame": ("frame_sync_kernelILi2ELi3008E", "frame_sym_kernelILb0ELi2E"),
+    "frame8": ("frame_sync_kernelILi0ELi0ELi4E", "frame_sym_kernelILb0ELi0E"),
 }
 
 

@@ -354,6 +354,7 @@ __device__ __forceinline__ int needed_k(int j) {
 #define FRAME_SYNC_WAVES 4
 #endif
 constexpr int SYM_THREADS = 256;    // frame_sym_kernel block: its items per block set the hand-off tile
+constexpr size_t FRAME_LDS_PER_CU = 160 * 1024;
 constexpr int SYNC_WAVES = FRAME_SYNC_WAVES;
 constexpr int SYNC_THREADS = 64 * SYNC_WAVES;
 constexpr int IMT_EXT = 128;         // table slack past one waveform copy: a lane's longest contiguous read
@@ -452,9 +453,10 @@ __host__ __device__ inline bool fr_in_capture(int cap_len, int n_data) {
 __host__ __device__ inline int wave_region_floats(int cap_len, int n_data) {
     return cap_region(cap_len) + (fr_in_capture(cap_len, n_data) ? 0 : 2 * fr_len(n_data));
 }
-__host__ __device__ inline size_t frame_lds_bytes(int cap_len, int n_data, int n_snr, int imt_len, int word_stats) {
+__host__ __device__ inline size_t frame_lds_bytes(int cap_len, int n_data, int n_snr, int imt_len, int word_stats,
+                                                  int waves = SYNC_WAVES) {
     return (size_t)n_snr * acc_slots(word_stats) * 8 + (((size_t)imt_len * 4 + 15) & ~size_t(15)) +
-           (size_t)SYNC_WAVES * wave_region_floats(cap_len, n_data) * 4;
+           (size_t)waves * wave_region_floats(cap_len, n_data) * 4;
 }
 
 // LDS ordering between the lanes of one wave (no block barrier: the other waves run other items)
@@ -554,9 +556,11 @@ __device__ __forceinline__ void capture_blocks(const A &a, int wave_len, float *
 // FIX_CAP samples generated from the waveform (no external capture, no dumps, no word-length statistics): the
 // reference message's sweep, with the detection rounds, table period, matched-filter runs and hand-off layout
 // folded by the compiler.  0, 0: everything from the arguments (any message, user captures, the parity dumps).
-template <int FIX_ND, int FIX_CAP>
-__global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kernel(FrameArgs a) {
+// W: waves per block (SYNC_WAVES; 1 for long captures, whose four-wave blocks would leave one block per CU).
+template <int FIX_ND, int FIX_CAP, int W = SYNC_WAVES>
+__global__ __launch_bounds__(64 * W, FRAME_SYNC_MINW) void frame_sync_kernel(FrameArgs a) {
     constexpr bool FIX = FIX_ND > 0;
+    constexpr int SYNC_WAVES = W, SYNC_THREADS = 64 * W;      // this instantiation's block
     static_assert(FIX == (FIX_CAP > 0), "both or neither");
     extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
     const int L = FIX ? FIX_CAP : a.cap_len, Lc = L - 47;       // Packet_Detection length (OFDM.c:663)
@@ -595,12 +599,16 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
     const int nwaves = (int)gridDim.x * SYNC_WAVES;
     int64_t run_end = ((int64_t)blockIdx.x * SYNC_WAVES + wv) * FRAME_ITEM_RUN + FRAME_ITEM_RUN;
     int nxt = 0;
+    int rs_run = 0;                       // lane l: the capture offset of item l of the current run
     for (int64_t i = run_end - FRAME_ITEM_RUN; i < a.n_items;) {
         // the kernel arguments are re-read per item (scalar loads through a pointer made opaque here)
         // instead of being hoisted into SGPRs held across the item loop, which spill
         using KArgs = const __attribute__((address_space(4))) FrameArgs;
         KArgs *ap = (KArgs *)__builtin_amdgcn_kernarg_segment_ptr();
-        asm volatile("" : "+s"(ap));
+#ifndef FRAME_FIX_OPAQUE
+#define FRAME_FIX_OPAQUE 1      // A/B option: 0 lets the fixed-geometry kernel hoist its arguments into SGPRs
+#endif
+        if (!FIX || FRAME_FIX_OPAQUE) asm volatile("" : "+s"(ap));
         KArgs &a = *ap;
         // the geometry: compile-time constants (FIX), or re-read per item with the arguments
         const int n_data = FIX ? FIX_ND : a.n_data;
@@ -631,9 +639,31 @@ __global__ __launch_bounds__(SYNC_THREADS, FRAME_SYNC_MINW) void frame_sync_kern
         const bool ext = !FIX && a.ext && first_item;
         // ---- capture window (OFDM.c:945-955) + AWGN: the real parts only ----
         int rx_start = a.fixed_start;
-        if (rx_start < 0) {
+        if (!FIX && rx_start < 0) {        // (the generic kernel has no VGPR to spare for the run's offsets)
             const uint4 o = philox10(t_lo, t_hi, 0u, STREAM_START | qs, a.k0, a.k1);
             rx_start = (int)(o.x % (uint32_t)(wave_len - L));
+        } else if (rx_start < 0) {
+            // the run's FRAME_ITEM_RUN capture offsets are drawn at its first item, lane l the offset of item l of
+            // the run (one Philox evaluation per run instead of one per item; the same draws)
+            const int k = (int)(i - (run_end - FRAME_ITEM_RUN));
+            if (k == 0) {
+                const int64_t gl = a.item0 + i + min(lane, FRAME_ITEM_RUN - 1);
+                int ql;
+                int64_t tl;
+                if ((uint64_t)(a.item0 + i + FRAME_ITEM_RUN) >> 32 == 0) {
+                    const uint32_t g32 = (uint32_t)gl, d = (uint32_t)a.n_snr;
+                    tl = g32 / d;
+                    ql = (int)(g32 - (uint32_t)tl * d);
+                } else {
+                    ql = (int)(gl % a.n_snr);
+                    tl = gl / a.n_snr;
+                }
+                const uint64_t tt = a.first_trial + (uint64_t)tl;
+                const uint4 o = philox10((uint32_t)tt, (uint32_t)(tt >> 32), 0u, STREAM_START | (uint32_t)(a.q_base + ql),
+                                         a.k0, a.k1);
+                rs_run = (int)(o.x % (uint32_t)(wave_len - L));
+            }
+            rx_start = __builtin_amdgcn_readlane(rs_run, k);
         }
         rx_start = __builtin_amdgcn_readfirstlane(rx_start);     // uniform: the capture geometry in SGPRs
         const int off = rx_start & 3;
@@ -1336,10 +1366,24 @@ static int run_frame_chunk(Ctx *c, FrameArgs &a) {
     const bool fixed = a.n_data == 2 && a.cap_len == cap_len_for(2) && a.wave_len == wave_len_for(2) && !a.ext &&
                        !a.dbg_res && !a.dbg_ints && !a.dbg_bits && !a.dbg_eq && !a.dbg_corr && !a.dbg_frame &&
                        !a.word_stats && !getenv("OFDM_FRAME_GENERIC");
+    // Long captures (8-symbol messages: 24 KB per wave) could run one-wave blocks, which fit five per CU where
+    // one four-wave block fits; but five waves on four SIMDs leave three SIMDs with one wave each, and
+    // the 8-symbol sweep measured 4.07e8 with one-wave blocks against 4.16e8 with four-wave ones (round 4,
+    // profiles/r04/ab/h_frame8*.json).  So one-wave blocks run only when they give every SIMD more waves:
+    // resident = whole waves per SIMD x 4, from W x floor(LDS per CU / block LDS), at most 12
+    const size_t lds1 = frame_lds_bytes(a.cap_len, a.n_data, a.n_snr, a.imt_len, a.word_stats, 1) + FRAME_LDS_PAD;
+    auto resident = [](size_t b, int w) {
+        return std::min<int64_t>(12, w * (int64_t)(FRAME_LDS_PER_CU / b) / 4 * 4);
+    };
+    const bool one = !fixed && ((resident(lds1, 1) > resident(lds, SYNC_WAVES) && !getenv("OFDM_FRAME_BLOCK4")) ||
+                                getenv("OFDM_FRAME_BLOCK1"));
     const void *ks = fixed ? reinterpret_cast<const void *>(&frame_sync_kernel<2, 3008>)
+                   : one   ? reinterpret_cast<const void *>(&frame_sync_kernel<0, 0, 1>)
                            : reinterpret_cast<const void *>(&frame_sync_kernel<0, 0>);
-    const dim3 gs(occupancy_grid(ks, SYNC_THREADS, lds, c->cus, (runs + SYNC_WAVES - 1) / SYNC_WAVES, 1));
+    const int waves = one ? 1 : SYNC_WAVES;
+    const dim3 gs(occupancy_grid(ks, 64 * waves, one ? lds1 : lds, c->cus, (runs + waves - 1) / waves, 1));
     if (fixed) hipLaunchKernelGGL((frame_sync_kernel<2, 3008>), gs, dim3(SYNC_THREADS), lds, c->stream, a);
+    else if (one) hipLaunchKernelGGL((frame_sync_kernel<0, 0, 1>), gs, dim3(64), lds1, c->stream, a);
     else hipLaunchKernelGGL((frame_sync_kernel<0, 0>), gs, dim3(SYNC_THREADS), lds, c->stream, a);
     const int ipb = (SYM_THREADS / 4) / ((a.n_data + 1) / 2);
     const bool dump = a.dbg_eq || a.dbg_bits || a.dbg_res;

@@ -216,7 +216,10 @@ static __device__ unsigned long long g_pack_stamps[4][8];
                             // profiles/r04/ab): c3 1.236 -> 1.260e10, c5 1.193 -> 1.220e10; 8 copies the same
 #endif
 #ifndef OFDM_PACK_SPEC_LIN
-#define OFDM_PACK_SPEC_LIN 1    // the prologue's clean-spectrum stores: a wave's lanes on consecutive frames (A/B)
+// A/B option: the prologue's clean-spectrum stores with a wave's lanes on consecutive frames (conflict-free LDS
+// stores, but each wave then reads every other symbol of the Tx rows): c3 -4.7 %, c5 -4 %, c2 +-0 (round 4,
+// profiles/r04/ab/ab_map.txt), so the 2-way store conflicts stay
+#define OFDM_PACK_SPEC_LIN 0
 #endif
 #ifndef PACK_SACC_SUB
 #define PACK_SACC_SUB 1     // the same for the ideal-CSI receiver (2 copies spill it at its 168-VGPR budget)

@@ -150,6 +150,23 @@ def test_fixed_geometry_kernel_equals_generic(engine, pkg, monkeypatch, no_lazy)
     assert fixed[0, 0] == 4000
 
 
+def test_long_message_one_wave_blocks_equal_four_wave_blocks(pkg, monkeypatch):
+    """An 8-symbol message's 5955-sample captures take 24 KB of LDS per wave: one four-wave block fits per CU,
+    five one-wave blocks would (measured slower, see run_frame_chunk).  The one-wave instantiation
+    (OFDM_FRAME_BLOCK1=1) gives every counter and packet_idx of the four-wave one."""
+    snrs = np.array([4.0, 10.0, 16.0, 30.0])
+    msg = (b"one-wave blocks for long messages " * 3)[:96]
+    with pkg.Engine(0) as e8:
+        assert e8.set_message(msg) == 8
+        cfg8 = pkg.make_cfg(payload="message")
+        four, p4 = e8.frame_sweep(cfg8, snrs, 3000, want_packet_idx=True)
+        monkeypatch.setenv("OFDM_FRAME_BLOCK1", "1")
+        one, p1 = e8.frame_sweep(cfg8, snrs, 3000, want_packet_idx=True)
+    assert np.array_equal(p1, p4)
+    assert np.array_equal(one, four)
+    assert np.mean(p1[2:] > 0) > 0.99
+
+
 def test_frame_sweep_two_chunks_equal_their_halves(engine, pkg):
     """A sweep of more than 2^22 (trial, SNR) items runs as several sync -> symbol launch pairs through the
     hand-off buffer: its counters and packet_idx equal those of two sweeps of half the trials each (one
