@@ -18,7 +18,8 @@ CSRC = PKG_DIR / "csrc"
 INCLUDE = PKG_DIR.parent / "include"
 BUILD = PKG_DIR / "_build"
 LIB = PKG_DIR / "libofdm_mi355x.so"
-SOURCES = ["ofdm_capi.hip", "ofdm_symbol.hip", "ofdm_rxpack.hip", "ofdm_rxpack_ideal.hip", "ofdm_frame.hip"]
+SOURCES = ["ofdm_capi.hip", "ofdm_symbol.hip", "ofdm_rxpack.hip", "ofdm_rxpack_ideal.hip", "ofdm_frame.hip",
+           "ofdm_frame_sym.hip"]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -fno-slp-vectorize: keep f32 math scalar (packed v_pk_* f32 gives no rate on gfx950 and its
@@ -35,7 +36,8 @@ CFLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-fno-slp-vecto
 SOURCE_FLAGS = {"ofdm_symbol.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
                 "ofdm_rxpack.hip": os.environ.get("OFDM_RXPACK_FLAGS", "-mllvm -amdgpu-sched-strategy=max-ilp").split(),
                 "ofdm_rxpack_ideal.hip": os.environ.get("OFDM_RXPACK_IDEAL_FLAGS", "").split(),
-                "ofdm_frame.hip": os.environ.get("OFDM_FRAME_FLAGS", "").split()}
+                "ofdm_frame.hip": os.environ.get("OFDM_FRAME_FLAGS", "").split(),
+                "ofdm_frame_sym.hip": os.environ.get("OFDM_FRAME_SYM_FLAGS", "").split()}
 
 
 # Kernels whose parity-dump variants (last template argument `true`) are allowed to spill: they

@@ -168,6 +168,7 @@ __global__ __launch_bounds__(256) void frame_wave_kernel(WaveArgs a) {
 // ======================================================================== K4c: over the air
 // Transmission_Over_Air (OFDM.c:635-655): P = mean|x|^2, sigma^2 = P/10^(snr/10), real-only noise
 // (D7), Gaussian k of stream (seed, trial, snr_index).
+#ifndef OFDM_FRAME_SYM_TU   // the non-template kernels live in this translation unit only
 __global__ __launch_bounds__(256) void power_kernel(const float2 *x, int n, double *out) {
     __shared__ double red[256];
     double s = 0.0;
@@ -200,6 +201,7 @@ __global__ __launch_bounds__(256) void ota_kernel(const float2 *x, float2 *y, in
         }
     }
 }
+#endif
 
 // ======================================================================== K4b: receiver
 __device__ __forceinline__ float wave_sum_f(float v) {
@@ -278,6 +280,7 @@ __device__ __forceinline__ float wave_max_f(float v) {
 
 // Word_Optimization_Analysis of one capture (OFDM.c:38-73): RRC matched filter over all n + 20
 // outputs (Convolution, OFDM.c:342-364), min / max of the real and imaginary parts -> out[0..1]
+#ifndef OFDM_FRAME_SYM_TU
 __global__ __launch_bounds__(256) void word_length_kernel(const float2 *x, int n, FrameArgs a, float *out) {
     __shared__ float smin[4], smax[4];
     float mn = 1e9f, mx = -1e9f;
@@ -303,6 +306,7 @@ __global__ __launch_bounds__(256) void word_length_kernel(const float2 *x, int n
         out[1] = fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3]));
     }
 }
+#endif
 
 // rotate by exp(-j 2 pi f Ts i): phase in revolutions evaluated in fp64 and range-reduced, so the
 // rotation matches OFDM.c:802,825 (double cexp of a float frequency) to fp32 rounding
@@ -1219,6 +1223,32 @@ __global__ __launch_bounds__(SYM_THREADS, FRAME_SYM_MINB) void frame_sym_kernel(
     }
 }
 
+static unsigned occupancy_grid(const void *kernel, int threads, size_t lds, int cus, int64_t blocks, int waves = 2) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, lds) != hipSuccess || per_cu < 1)
+        per_cu = 2;
+    return (unsigned)std::max<int64_t>(1, std::min<int64_t>(blocks, (int64_t)per_cu * cus * waves));
+}
+
+#ifdef OFDM_FRAME_SYM_TU
+// K4b' (frame_sym_kernel) is instantiated in its own translation unit (ofdm_frame_sym.hip) so that the sync
+// kernel's can be compiled with another scheduler (build_lib.SOURCE_FLAGS); this is its launcher.
+void launch_frame_sym(hipStream_t st, const FrameArgs &a, int cus) {
+    const int ipb = (SYM_THREADS / 4) / ((a.n_data + 1) / 2);
+    const bool dump = a.dbg_eq || a.dbg_bits || a.dbg_res;
+    const bool sym2 = a.n_data == 2 && !getenv("OFDM_FRAME_GENERIC");     // the hand-off offsets folded
+    const void *k = dump ? reinterpret_cast<const void *>(&frame_sym_kernel<true, 0>)
+                  : sym2 ? reinterpret_cast<const void *>(&frame_sym_kernel<false, 2>)
+                         : reinterpret_cast<const void *>(&frame_sym_kernel<false, 0>);
+    const dim3 grid(occupancy_grid(k, SYM_THREADS, 0, cus, (a.n_items + ipb - 1) / ipb));
+    if (dump) hipLaunchKernelGGL((frame_sym_kernel<true, 0>), grid, dim3(SYM_THREADS), 0, st, a);
+    else if (sym2) hipLaunchKernelGGL((frame_sym_kernel<false, 2>), grid, dim3(SYM_THREADS), 0, st, a);
+    else hipLaunchKernelGGL((frame_sym_kernel<false, 0>), grid, dim3(SYM_THREADS), 0, st, a);
+}
+}  // namespace ofdm
+#else
+void launch_frame_sym(hipStream_t st, const FrameArgs &a, int cus);     // ofdm_frame_sym.hip
+
 // ======================================================================== host side
 // rcosdesign(0.5, 10, 2, 'sqrt') (Tester.m:112; OFDM.c:32 holds the same values as floats)
 static void rrc_taps(float out[21]) {
@@ -1314,13 +1344,6 @@ static int32_t word_bits(double mn, double mx) {
     return max_abs < 1.0f ? 1 : (int32_t)std::ceil(std::log2((double)max_abs)) + 1;
 }
 
-static unsigned occupancy_grid(const void *kernel, int threads, size_t lds, int cus, int64_t blocks, int waves = 2) {
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, lds) != hipSuccess || per_cu < 1)
-        per_cu = 2;
-    return (unsigned)std::max<int64_t>(1, std::min<int64_t>(blocks, (int64_t)per_cu * cus * waves));
-}
-
 // items per sync -> symbol hand-off: 2^22 items x 2 KB (reference message) = 8 GB of HBM, one launch pair per
 // 4M items (A/B, frame mode: 2^18 3.13e8, 2^20 3.33e8, 2^22 3.40e8 symbol-SNR/s -- each pair ends in a tail
 // and K4b' waits for K4b)
@@ -1385,16 +1408,7 @@ static int run_frame_chunk(Ctx *c, FrameArgs &a) {
     if (fixed) hipLaunchKernelGGL((frame_sync_kernel<2, 3008>), gs, dim3(SYNC_THREADS), lds, c->stream, a);
     else if (one) hipLaunchKernelGGL((frame_sync_kernel<0, 0, 1>), gs, dim3(64), lds1, c->stream, a);
     else hipLaunchKernelGGL((frame_sync_kernel<0, 0>), gs, dim3(SYNC_THREADS), lds, c->stream, a);
-    const int ipb = (SYM_THREADS / 4) / ((a.n_data + 1) / 2);
-    const bool dump = a.dbg_eq || a.dbg_bits || a.dbg_res;
-    const bool sym2 = a.n_data == 2 && !getenv("OFDM_FRAME_GENERIC");     // the hand-off offsets folded
-    const void *k = dump ? reinterpret_cast<const void *>(&frame_sym_kernel<true, 0>)
-                  : sym2 ? reinterpret_cast<const void *>(&frame_sym_kernel<false, 2>)
-                         : reinterpret_cast<const void *>(&frame_sym_kernel<false, 0>);
-    const dim3 grid(occupancy_grid(k, SYM_THREADS, 0, c->cus, (a.n_items + ipb - 1) / ipb));
-    if (dump) hipLaunchKernelGGL((frame_sym_kernel<true, 0>), grid, dim3(SYM_THREADS), 0, c->stream, a);
-    else if (sym2) hipLaunchKernelGGL((frame_sym_kernel<false, 2>), grid, dim3(SYM_THREADS), 0, c->stream, a);
-    else hipLaunchKernelGGL((frame_sym_kernel<false, 0>), grid, dim3(SYM_THREADS), 0, c->stream, a);
+    launch_frame_sym(c->stream, a, c->cus);
     HIPOK(hipGetLastError());
     return OFDM_OK;
 }
@@ -1599,3 +1613,4 @@ int ofdm_word_length_report(ofdm_ctx *ctx, const float *capture, int32_t cap_len
 }
 
 }  // extern "C"
+#endif  // OFDM_FRAME_SYM_TU

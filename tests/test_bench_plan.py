@@ -1,6 +1,7 @@
 """bench.py's step plan (CPU) and its pipelined symbol step against one ofdm_symbol_sweep (GPU): the
 benchmark's own code path must produce the counters a plain sweep produces."""
 import importlib.util
+import json
 import sys
 
 import numpy as np
@@ -360,3 +361,42 @@ def test_pipelined_ideal_step_equals_symbol_sweep(engine, pkg):
         torch.cuda.synchronize()
         want = engine.symbol_sweep(cfg, b.SNR_GRID, frames, first_frame=first)
         assert np.array_equal(counters.cpu().numpy(), want)
+
+
+def test_trace_frac_keeps_the_timed_launches(tmp_path):
+    """tools/trace_frac.py: from a rocprofv3 kernel trace of the bench command, the receiver dispatches of the
+    timed steps only (warm-up first, in dispatch order), summed per bench launch, priced as bench.make_roofline."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("trace_frac", ROOT / "tools" / "trace_frac.py")
+    tf = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(tf)
+    d = tmp_path / "trace"
+    d.mkdir()
+    rows = ["Kind,Dispatch_Id,Kernel_Name,Start_Timestamp,End_Timestamp"]
+    t, did = 0, 0
+    # 2 warm-up + 3 timed steps of a frame-like launch: 2 chunks x (sync, sym) per step, one bench launch per step
+    for step in range(5):
+        for chunk in range(2):
+            for k, dur in (("ofdm::frame_sync_kernel<2, 3008, 4>(ofdm::FrameArgs)", 900 if step < 2 else 1000),
+                           ("void ofdm::frame_sym_kernel<false, 2>(ofdm::FrameArgs)", 100)):
+                did += 1
+                rows.append(f'KERNEL_DISPATCH,{did},"{k}",{t},{t + dur}')
+                t += dur + 10
+            did += 1
+            rows.append(f'KERNEL_DISPATCH,{did},"__amd_rocclr_fillBufferAligned",{t},{t + 5}')
+    (d / "run_kernel_trace.csv").write_text("\n".join(rows) + "\n")
+    line = {"steps": 3, "warmup": 2, "roofline": {"kernel": "frame_sync_kernel+frame_sym_kernel", "launches": 3,
+                                                  "units_per_launch": 1e6, "instr_per_unit": 10.0, "peak": 1e12,
+                                                  "frac": 0.0045, "avg_launch_ms": 0.0022}}
+    b = tmp_path / "line.json"
+    b.write_text(json.dumps(line) + "\n")
+    rec, per = tf.split(tf.receiver_dispatches(d, "frame_sync_kernel+frame_sym_kernel"), line)
+    assert per == 4 and len(rec) == 12
+    ns = tf.launch_ns(rec, per)
+    assert ns == [2200, 2200, 2200]                       # the warm-up's 900-ns sync dispatches are dropped
+    out = tmp_path / "frac.json"
+    tf.main([str(d), str(b), "--out", str(out)])
+    r = json.loads(out.read_text())
+    assert r["trace_frac"] == pytest.approx(1e6 * 10.0 / 2.2e-6 / 1e12)
+    # the line's own HIP-event mean launch time (2.2 us here) prices the same: no difference
+    assert r["line_events_frac"] == pytest.approx(r["trace_frac"]) and abs(r["frac_rel_diff"]) < 1e-9

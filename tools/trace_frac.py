@@ -18,6 +18,7 @@ import sys
 from pathlib import Path
 
 XCDS = 8
+ROOT = Path(__file__).resolve().parents[1]
 
 
 def receiver_dispatches(trace_dir: Path, kernel: str) -> list[dict]:
@@ -66,6 +67,13 @@ def main(argv):
     line = json.loads(bench.read_text().strip().splitlines()[-1])
     rf = line["roofline"]
     kernel, upl, ipu = rf["kernel"], rf["units_per_launch"], rf.get("instr_per_unit")
+    pmc_src = "the line's certified PMC record"
+    if not ipu:       # the line predates its PMC record: take the record of the same build (same kernel id)
+        wl = line["config"]["workload"]
+        rec = json.loads((ROOT / "profiles" / "pmc_summary.json").read_text()).get({"c4": "c3"}.get(wl, wl), {})
+        if rec.get("build_id") and rec.get("build_id") == rf.get("lib_build_id"):
+            ipu = rec["valu_instr_per_unit"]
+            pmc_src = f"profiles/pmc_summary.json[{wl}] (build {rec['build_id']} = the line's library)"
     rows, per_launch = split(receiver_dispatches(trace_dir, kernel), line)
     ns = launch_ns(rows, per_launch)
     avg_s = sum(ns) / len(ns) * 1e-9
@@ -75,8 +83,10 @@ def main(argv):
            "trace_avg_launch_ms": avg_s * 1e3, "line_avg_launch_ms": rf["avg_launch_ms"],
            "line_frac": rf.get("frac")}
     if ipu:
+        out["instr_per_unit"], out["pmc_source"] = ipu, pmc_src
         out["trace_frac"] = upl * ipu / avg_s / rf["peak"]
-        out["frac_rel_diff"] = out["trace_frac"] / rf["frac"] - 1 if rf.get("frac") else None
+        out["line_events_frac"] = upl * ipu / (rf["avg_launch_ms"] * 1e-3) / rf["peak"]
+        out["frac_rel_diff"] = out["trace_frac"] / out["line_events_frac"] - 1
     if "--clock" in argv:
         out["clock_ghz"] = clock_ghz(Path(argv[argv.index("--clock") + 1]), kernel, line)
     text = json.dumps(out, indent=1)
