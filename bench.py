@@ -98,6 +98,11 @@ def issue_cap(pmc: dict, frac: float) -> dict:
                 "issue_model_note": "cap = 2 x VALU / SIMD cycles of the dynamic class mix (PMC class counters) at "
                                     "%d waves/SIMD, unclassified instructions priced slow (cap) or fast (upper end)"
                                     % m["waves_per_simd"]}
+    if m.get("method") == "classified":  # tools/frame_mix.py: every VALU instruction classified, blocks weighted
+        return {"issue_model_cap_frac": m["cap_frac"], "frac_of_issue_model_cap": frac / m["cap_frac"],
+                "issue_model_note": "cap = 2 x VALU / class-priced SIMD cycles at %d waves/SIMD of both kernels' "
+                                    "assembly, blocks weighted per item (undecided fraction %.3f fitted to the "
+                                    "measured SQ_INSTS_VALU)" % (m["waves_per_simd"], m["undecided_fraction"])}
     return {"issue_model_cap_frac": m["cap_frac"], "frac_of_issue_model_cap": frac / m["cap_frac"],
             "issue_model_note": "cap = 2 x loop VALU / class-priced SIMD cycles at %d waves/SIMD (modelled)"
                                 % m["waves_per_simd"]}

@@ -153,6 +153,34 @@ def test_dynamic_mix_cap(tmp_path):
     assert cap["frac_of_issue_model_cap_range"] == pytest.approx([0.5 / hi, 0.5 / lo])
 
 
+def test_classified_frame_cap(tmp_path):
+    """tools/frame_mix.py finds the sync kernel's phases in the current gfx950 assembly (round-0 capture passes,
+    the per-run offsets, the blocks round 0's decision skips), recovers the undecided fraction from a VALU count
+    made with it, and bench.py reports one cap number for the classified record."""
+    sys.path.insert(0, str(ROOT / "tools"))
+    import frame_mix
+    sync_text, sym_text = frame_mix.asm("ofdm_frame.hip"), frame_mix.asm("ofdm_frame_sym.hip")
+    sbb = frame_mix.kernel_blocks(sync_text, frame_mix.SYNC)
+    w = frame_mix.weights(sbb, 2.0)
+    assert sum(1 for a, b in w.values() if b) >= 5                # the undecided path spans several blocks
+    assert any(0 < a < 1 for a, b in w.values())                  # the per-run offsets
+    cls, _, _ = frame_mix.tally(sbb, w)
+    items, u = 1000.0, 0.4
+    d = tmp_path / "pass"
+    d.mkdir()
+    with open(d / "run_counter_collection.csv", "w") as f:
+        f.write("Kernel_Name,Counter_Name,Counter_Value\n")
+        f.write(f"\"ofdm::frame_sync_kernel<2, 3008, 4>(ofdm::FrameArgs)\",SQ_INSTS_VALU,"
+                f"{items * (cls['valu'][0] + u * cls['valu'][1])}\n")
+        f.write(f"\"ofdm::frame_sym_kernel<false, 2>(ofdm::FrameArgs)\",SQ_INSTS_VALU,{items * 130}\n")
+    m = frame_mix.model([d], items, 3, sync_text, sym_text)
+    assert m["undecided_fraction"] == pytest.approx(u)
+    assert 0.5 < m["sync"]["cap_frac"] < 0.9 and 0.5 < m["cap_frac"] < 0.9
+    cap = _bench().issue_cap({"issue_model": {"method": "classified", "cap_frac": m["cap_frac"], "waves_per_simd": 3,
+                                              "undecided_fraction": u}}, 0.5)
+    assert cap["issue_model_cap_frac"] == m["cap_frac"] and "issue_model_cap_frac_range" not in cap
+
+
 def test_kernel_build_id_tracks_code_bytes(pkg, tmp_path):
     """The id is a hash of the kernel's machine code: flipping one byte of it in a copy of the library
     changes the id of that workload and no other's."""
