@@ -23,6 +23,12 @@
 #include <cstring>
 #include <vector>
 
+// ofdm_frame_sym.hip / ofdm_frame_fix.hip include this file to instantiate one kernel each in a translation unit of
+// its own (their own scheduler flags, build_lib.SOURCE_FLAGS); everything else lives in this one
+#if defined(OFDM_FRAME_SYM_TU) || defined(OFDM_FRAME_FIX_TU)
+#define OFDM_FRAME_AUX_TU 1
+#endif
+
 namespace ofdm {
 
 // frame geometry for nd data symbols (OFDM.c:569-612, 945): [STF 160 | LTF 160 | nd x 80]
@@ -85,7 +91,30 @@ struct FrameArgs {
     int32_t add_totals;             // 1 on the last chunk: add frames / symbols / bits / terms
     unsigned long long *work;       // sync kernel: items handed out past the first gridDim.x (zeroed per launch)
     int32_t region_floats;          // LDS floats per wave (wave_region_floats)
+    // item0 = trial0 n_snr + q0: chunk item i is trial trial0 + (q0 + i) / n_snr, SNR (q0 + i) % n_snr, a 32-bit
+    // division by one multiply-high with snr_magic = floor((2^32 - 1) / n_snr) (snr_divmod; run_frame_chunk)
+    int64_t trial0;
+    int32_t q0;
+    uint32_t snr_magic;
 };
+
+// x / d and x % d for 32-bit x and d >= 1: with m = floor((2^32 - 1) / d) >= (2^32 - d) / d,
+// x / d - 1 < x / d - x / 2^32 <= x m / 2^32 <= x / d, so t = mulhi(x, m) is the quotient or one less and one
+// correction step finishes it.  On wave-uniform operands it stays on the scalar unit (the compiler's udiv
+// expansion goes through VALU float reciprocals, and was re-done per item)
+__host__ __device__ __forceinline__ uint32_t snr_divmod(uint32_t x, uint32_t d, uint32_t magic, uint32_t &r) {
+#ifdef __HIP_DEVICE_COMPILE__
+    uint32_t t = __umulhi(x, magic);
+#else
+    uint32_t t = (uint32_t)(((uint64_t)x * magic) >> 32);
+#endif
+    r = x - t * d;
+    if (r >= d) {
+        ++t;
+        r -= d;
+    }
+    return t;
+}
 
 #ifdef OFDM_FRAME_STAMPS   // diagnostic build: s_memtime per phase, summed over the grid
 #define FR_STAMP(k)                                                                  \
@@ -99,6 +128,7 @@ struct FrameArgs {
 #endif
 
 // ======================================================================== K4a: waveform
+#ifndef OFDM_FRAME_AUX_TU
 template <int CONV>
 __global__ __launch_bounds__(256) void frame_wave_kernel(WaveArgs a) {
     __shared__ float2 T[2 + FR_MAX_DATA][64];   // STF, LTF, data time symbols
@@ -164,11 +194,12 @@ __global__ __launch_bounds__(256) void frame_wave_kernel(WaveArgs a) {
     }
     if (tid == 0) *a.power = red[0] / nfilt;      // mean over 10 identical repeats
 }
+#endif
 
 // ======================================================================== K4c: over the air
 // Transmission_Over_Air (OFDM.c:635-655): P = mean|x|^2, sigma^2 = P/10^(snr/10), real-only noise
 // (D7), Gaussian k of stream (seed, trial, snr_index).
-#ifndef OFDM_FRAME_SYM_TU   // the non-template kernels live in this translation unit only
+#ifndef OFDM_FRAME_AUX_TU   // the non-template kernels live in this translation unit only
 __global__ __launch_bounds__(256) void power_kernel(const float2 *x, int n, double *out) {
     __shared__ double red[256];
     double s = 0.0;
@@ -280,7 +311,7 @@ __device__ __forceinline__ float wave_max_f(float v) {
 
 // Word_Optimization_Analysis of one capture (OFDM.c:38-73): RRC matched filter over all n + 20
 // outputs (Convolution, OFDM.c:342-364), min / max of the real and imaginary parts -> out[0..1]
-#ifndef OFDM_FRAME_SYM_TU
+#ifndef OFDM_FRAME_AUX_TU
 __global__ __launch_bounds__(256) void word_length_kernel(const float2 *x, int n, FrameArgs a, float *out) {
     __shared__ float smin[4], smax[4];
     float mn = 1e9f, mx = -1e9f;
@@ -505,7 +536,8 @@ __device__ __forceinline__ void capture_blocks(const A &a, int wave_len, float *
     const PhiloxHead hd = philox_head(t_lo, t_hi, STREAM_NOISE | qs, a.k1);
     const float Ksig = noise_k(sigma);
     // round keys in VGPRs: each round's two v_bitop3_b32 issue at the fast rate (an SGPR operand makes
-    // them slow-class); 20 VGPRs for the capture loop only
+    // them slow-class); 20 VGPRs for the capture loop only (held across the item loop instead, in
+    // the fixed-geometry kernel, they spill one VGPR)
     PhiloxKeysV vk;
     vk.init(a.k0, a.k1);
     // Gaussian k of the trial's stream goes to waveform sample k (as if Transmission_Over_Air had drawn
@@ -626,16 +658,9 @@ __global__ __launch_bounds__(64 * W, FRAME_SYNC_MINW) void frame_sync_kernel(Fra
         const bool fr_in_cap = FIX ? fr_in_capture(FIX_CAP, FIX_ND) : a.fr_in_cap;
         if (lane == 0 && i == run_end - FRAME_ITEM_RUN) nxt = nwaves + (int)atomicAdd(a.work, 1ull);
         const int64_t g = a.item0 + i;
-        int q;
-        int64_t ti;
-        if ((uint64_t)g >> 32 == 0) {        // 32-bit division while it fits
-            const uint32_t g32 = (uint32_t)g, d = (uint32_t)a.n_snr;
-            ti = g32 / d;
-            q = (int)(g32 - (uint32_t)ti * d);
-        } else {
-            q = (int)(g % a.n_snr);
-            ti = g / a.n_snr;
-        }
+        uint32_t qr;
+        const int64_t ti = a.trial0 + snr_divmod((uint32_t)a.q0 + (uint32_t)i, (uint32_t)a.n_snr, a.snr_magic, qr);
+        const int q = (int)qr;
         const uint64_t t = a.first_trial + (uint64_t)ti;
         const uint32_t t_lo = (uint32_t)t, t_hi = (uint32_t)(t >> 32), qs = (uint32_t)(a.q_base + q);
         const float sigma = a.sigma[q];
@@ -651,19 +676,11 @@ __global__ __launch_bounds__(64 * W, FRAME_SYNC_MINW) void frame_sync_kernel(Fra
             // the run (one Philox evaluation per run instead of one per item; the same draws)
             const int k = (int)(i - (run_end - FRAME_ITEM_RUN));
             if (k == 0) {
-                const int64_t gl = a.item0 + i + min(lane, FRAME_ITEM_RUN - 1);
-                int ql;
-                int64_t tl;
-                if ((uint64_t)(a.item0 + i + FRAME_ITEM_RUN) >> 32 == 0) {
-                    const uint32_t g32 = (uint32_t)gl, d = (uint32_t)a.n_snr;
-                    tl = g32 / d;
-                    ql = (int)(g32 - (uint32_t)tl * d);
-                } else {
-                    ql = (int)(gl % a.n_snr);
-                    tl = gl / a.n_snr;
-                }
-                const uint64_t tt = a.first_trial + (uint64_t)tl;
-                const uint4 o = philox10((uint32_t)tt, (uint32_t)(tt >> 32), 0u, STREAM_START | (uint32_t)(a.q_base + ql),
+                uint32_t ql;
+                const uint32_t tl = snr_divmod((uint32_t)a.q0 + (uint32_t)i + (uint32_t)min(lane, FRAME_ITEM_RUN - 1),
+                                               (uint32_t)a.n_snr, a.snr_magic, ql);
+                const uint64_t tt = a.first_trial + (uint64_t)(a.trial0 + tl);
+                const uint4 o = philox10((uint32_t)tt, (uint32_t)(tt >> 32), 0u, STREAM_START | (uint32_t)(a.q_base + (int)ql),
                                          a.k0, a.k1);
                 rs_run = (int)(o.x % (uint32_t)(wave_len - L));
             }
@@ -1181,7 +1198,8 @@ __global__ __launch_bounds__(SYM_THREADS, FRAME_SYM_MINB) void frame_sym_kernel(
                     fe += part_e[quad + k][r2]; ferr += part_b[quad + k][r2]; fax += part_a[quad + k][r2];
                 }
             const int64_t g = a.item0 + i;
-            const int q = (int)(g % a.n_snr);
+            uint32_t q;
+            (void)snr_divmod((uint32_t)a.q0 + (uint32_t)i, (uint32_t)a.n_snr, a.snr_magic, q);
             unsigned long long *sl = acc[q];
             atomicAdd(&sl[0], (unsigned long long)ferr);
             atomicAdd(&sl[1], (unsigned long long)(ferr > 0u));
@@ -1246,8 +1264,19 @@ void launch_frame_sym(hipStream_t st, const FrameArgs &a, int cus) {
     else hipLaunchKernelGGL((frame_sym_kernel<false, 0>), grid, dim3(SYM_THREADS), 0, st, a);
 }
 }  // namespace ofdm
+#elif defined(OFDM_FRAME_FIX_TU)
+// K4b with the reference message's geometry folded (frame_sync_kernel<2, 3008>) in its own translation unit
+// (ofdm_frame_fix.hip), scheduled for ILP without spilling the generic instantiations (A/B +0.4 %,
+// profiles/r04/ab/q_ab_syncilp.txt); its occupancy handle and launcher
+const void *frame_fix_kernel() { return reinterpret_cast<const void *>(&frame_sync_kernel<2, 3008>); }
+void launch_frame_fix(hipStream_t st, const FrameArgs &a, dim3 grid, size_t lds) {
+    hipLaunchKernelGGL((frame_sync_kernel<2, 3008>), grid, dim3(SYNC_THREADS), lds, st, a);
+}
+}  // namespace ofdm
 #else
 void launch_frame_sym(hipStream_t st, const FrameArgs &a, int cus);     // ofdm_frame_sym.hip
+const void *frame_fix_kernel();                                         // ofdm_frame_fix.hip
+void launch_frame_fix(hipStream_t st, const FrameArgs &a, dim3 grid, size_t lds);
 
 // ======================================================================== host side
 // rcosdesign(0.5, 10, 2, 'sqrt') (Tester.m:112; OFDM.c:32 holds the same values as floats)
@@ -1361,6 +1390,11 @@ constexpr int64_t FRAME_CHUNK_MIN = int64_t(1) << 16;    // halving stops here w
 // K4b then K4b' over a.n_items items starting at a.item0, through the context's hand-off buffer
 static int run_frame_chunk(Ctx *c, FrameArgs &a) {
     const int nw = 2 + a.n_data;
+    if (a.n_snr < 1 || a.n_items < 0 || a.n_items + a.n_snr + FRAME_ITEM_RUN > (int64_t(1) << 31))
+        return set_error(OFDM_E_ARG, "frame chunk: items or SNR points out of range");
+    a.trial0 = a.item0 / a.n_snr;
+    a.q0 = (int32_t)(a.item0 % a.n_snr);
+    a.snr_magic = 0xFFFFFFFFu / (uint32_t)a.n_snr;
     a.ipb = (SYM_THREADS / 4) / ((a.n_data + 1) / 2);
     const size_t wbytes = (size_t)((a.n_items + a.ipb - 1) / a.ipb) * a.ipb * nw * 64 * sizeof(float2);
     int rc = c->ensure(&c->d_scratch, &c->cap_scratch, wbytes + (size_t)a.n_items * sizeof(int4) + 256);
@@ -1400,12 +1434,12 @@ static int run_frame_chunk(Ctx *c, FrameArgs &a) {
     };
     const bool one = !fixed && ((resident(lds1, 1) > resident(lds, SYNC_WAVES) && !getenv("OFDM_FRAME_BLOCK4")) ||
                                 getenv("OFDM_FRAME_BLOCK1"));
-    const void *ks = fixed ? reinterpret_cast<const void *>(&frame_sync_kernel<2, 3008>)
+    const void *ks = fixed ? frame_fix_kernel()
                    : one   ? reinterpret_cast<const void *>(&frame_sync_kernel<0, 0, 1>)
                            : reinterpret_cast<const void *>(&frame_sync_kernel<0, 0>);
     const int waves = one ? 1 : SYNC_WAVES;
     const dim3 gs(occupancy_grid(ks, 64 * waves, one ? lds1 : lds, c->cus, (runs + waves - 1) / waves, 1));
-    if (fixed) hipLaunchKernelGGL((frame_sync_kernel<2, 3008>), gs, dim3(SYNC_THREADS), lds, c->stream, a);
+    if (fixed) launch_frame_fix(c->stream, a, gs, lds);
     else if (one) hipLaunchKernelGGL((frame_sync_kernel<0, 0, 1>), gs, dim3(64), lds1, c->stream, a);
     else hipLaunchKernelGGL((frame_sync_kernel<0, 0>), gs, dim3(SYNC_THREADS), lds, c->stream, a);
     launch_frame_sym(c->stream, a, c->cus);
@@ -1613,4 +1647,4 @@ int ofdm_word_length_report(ofdm_ctx *ctx, const float *capture, int32_t cap_len
 }
 
 }  // extern "C"
-#endif  // OFDM_FRAME_SYM_TU
+#endif  // OFDM_FRAME_AUX_TU

@@ -159,7 +159,7 @@ def test_classified_frame_cap(tmp_path):
     made with it, and bench.py reports one cap number for the classified record."""
     sys.path.insert(0, str(ROOT / "tools"))
     import frame_mix
-    sync_text, sym_text = frame_mix.asm("ofdm_frame.hip"), frame_mix.asm("ofdm_frame_sym.hip")
+    sync_text, sym_text = frame_mix.asm("ofdm_frame_fix.hip"), frame_mix.asm("ofdm_frame_sym.hip")
     sbb = frame_mix.kernel_blocks(sync_text, frame_mix.SYNC)
     w = frame_mix.weights(sbb, 2.0)
     assert sum(1 for a, b in w.values() if b) >= 5                # the undecided path spans several blocks

@@ -5,7 +5,7 @@ detection round -- fitted to the measured SQ_INSTS_VALU of the sync kernel.
 
 usage: python tools/frame_mix.py <pmc dir>... [--items N] [--waves 3] [--record]
 
-The assembly is compiled here from the library's sources with build_lib's flags (ofdm_frame.hip for the sync
+The assembly is compiled here from the library's sources with build_lib's flags (ofdm_frame_fix.hip for the sync
 kernel, ofdm_frame_sym.hip for the symbol kernel), so run it on the tree that built the profiled library;
 --record takes the build id from the PMC run's kernel_ids.json (tools/gpu_profile.sh) and stores the cap as
 profiles/pmc_summary.json["frame"]["issue_model"] (method "classified") and profiles/frame_mix.json.
@@ -59,13 +59,15 @@ def asm(src: str) -> list[str]:
 
 
 def blocks(lines):
-    """[(name, loop depth, [(op, args)])] of a kernel body"""
+    """[(name, loop depth, [(op, args)], innermost loop header)] of a kernel body (the header from LLVM's
+    "in Loop: Header=BBk_n Depth=d" comments)"""
     out, cur = [], None
     for l in lines:
         m = re.match(r"^(\.LBB\w+|; %bb\.\d+):?(.*)", l)
         if m:
             d = re.search(r"Depth=(\d+)", m.group(2))
-            cur = [m.group(1), int(d.group(1)) if d else 0, []]
+            h = re.search(r"Header=(\w+)", m.group(2))
+            cur = [m.group(1), int(d.group(1)) if d else 0, [], h.group(1) if h else None]
             out.append(cur)
             continue
         t = l.strip().split(None, 1)
@@ -83,17 +85,6 @@ def kernel_blocks(text: list[str], name: str):
 
 def weights(bbs, passes0: float, run: int = 4):
     """per-item weight of each sync-kernel block as (constant, coefficient of u), u = 1 - decided"""
-    # the blocks inside the item loop: those between the first and the last depth >= 1 block
-    inner = [i for i, b in enumerate(bbs) if b[1] >= 1]
-    lo, hi = inner[0], inner[-1]
-    philox = [i for i in range(lo, hi + 1) if bbs[i][1] == 2 and sum(op == "v_mad_u64_u32" for op, _ in bbs[i][2]) >= 40]
-    detect = [i for i in range(lo, hi + 1) if sum(op == "v_alignbit_b32" for op, _ in bbs[i][2]) >= 10]
-    assert len(philox) == 2 and len(detect) == 2, (philox, detect)
-    w = {}
-    for i in range(lo, hi + 1):
-        w[i] = (1.0, 0.0)
-        if bbs[i][1] >= 3:
-            w[i] = (0.0, 0.0)                                   # per-instant matched-filter fallback
     label = {b[0]: i for i, b in enumerate(bbs)}
 
     def target(i, op):
@@ -101,12 +92,34 @@ def weights(bbs, passes0: float, run: int = 4):
         t = [a for o, a in bbs[i][2] if o == op]
         return label.get(t[0].strip()) if t else None
 
-    # the run's capture offsets (k == 0, a uniform branch over the first item of each run): the first forward
-    # s_cbranch_scc1 of the item loop that skips more than a few blocks before the capture passes
-    r0 = next(i for i in range(lo, philox[0]) if (target(i, "s_cbranch_scc1") or 0) > i + 5)
+    def back_edges(i):
+        """targets of the block i's backward branches"""
+        return [label[a.strip()] for o, a in bbs[i][2]
+                if o.startswith(("s_branch", "s_cbranch")) and a.strip() in label and label[a.strip()] <= i]
+
+    philox = [i for i, b in enumerate(bbs) if b[1] == 2 and sum(op == "v_mad_u64_u32" for op, _ in b[2]) >= 40]
+    detect = [i for i, b in enumerate(bbs) if sum(op == "v_alignbit_b32" for op, _ in b[2]) >= 10]
+    assert len(philox) == 2 and len(detect) == 2, (philox, detect)
+
+    # the item loop: the outermost loop around the capture passes (its back edge from the last latch)
+    lo, hi = min(((h, l) for l in range(philox[0], len(bbs)) for h in back_edges(l) if h <= philox[0]),
+                 key=lambda hl: hl[0])
+    w = {}
+    for i in range(lo, hi + 1):
+        w[i] = (1.0, 0.0)
+        if bbs[i][1] >= 3:
+            w[i] = (0.0, 0.0)                                   # per-instant matched-filter fallback
+    # the run's capture offsets (k == 0, a uniform branch over the first item of each run): the item-loop block
+    # holding a whole philox10 before the capture passes, and the blocks the nearest uniform branch over it skips
+    pr = next(i for i in range(lo, philox[0])
+              if bbs[i][1] == 1 and sum(op in ("v_mad_u64_u32", "v_mul_hi_u32") for op, _ in bbs[i][2]) >= 15)
+    r0 = next(i for i in range(pr - 1, lo - 1, -1) if (target(i, "s_cbranch_scc1") or 0) > pr)
     for i in range(r0 + 1, target(r0, "s_cbranch_scc1")):
         w[i] = (1.0 / run, 0.0)
-    w[philox[0]] = (passes0, 0.0)
+    # round 0's capture-pass loop: every block of it (the blocks LLVM annotates with its header) once per pass
+    for i in range(lo, hi + 1):
+        if bbs[i][3] == bbs[philox[0]][3] and bbs[i][1] == bbs[philox[0]][1]:
+            w[i] = (passes0, 0.0)
     # round 0 decided: the uniform branch after the round-0 detection that jumps past round 1 and the
     # undecided Packet_Selection; every block it skips is on the undecided path
     d0 = next(i for i in range(detect[0] + 1, philox[1]) if (target(i, "s_cbranch_vccnz") or 0) > detect[1])
@@ -153,7 +166,7 @@ def pmc(dirs, kernel_frag):
 
 
 def model(dirs, items: float, waves: int, sync_text=None, sym_text=None) -> dict:
-    sbb = kernel_blocks(sync_text or asm("ofdm_frame.hip"), SYNC)
+    sbb = kernel_blocks(sync_text or asm("ofdm_frame_fix.hip"), SYNC)
     cls, dyn, ops = tally(sbb, weights(sbb, 2.0))
     ybb = kernel_blocks(sym_text or asm("ofdm_frame_sym.hip"), SYM)
     ycls, _, _ = tally(ybb, {i: (1.0, 0.0) for i, b in enumerate(ybb) if b[1] >= 1})

@@ -37,16 +37,26 @@ def kernel_key(name):
 
 
 def read_counters(d: Path):
-    sums = defaultdict(lambda: defaultdict(float))     # kernel -> counter -> sum over dispatches
+    """kernel -> counter -> sum over dispatches (and dispatch counts); a counter collected in several passes
+    (SQ_INSTS_VALU beside each class group) is taken from the first pass that holds it (pmc_1, pmc_2, ...)"""
+    sums = defaultdict(lambda: defaultdict(float))
     n = defaultdict(lambda: defaultdict(int))
-    for f in sorted(d.glob("pmc_*/**/*counter_collection.csv")):
-        with open(f) as fh:
-            for r in csv.DictReader(fh):
-                k = kernel_key(r["Kernel_Name"])
-                if not k:
-                    continue
-                sums[k][r["Counter_Name"]] += float(r["Counter_Value"])
-                n[k][r["Counter_Name"]] += 1
+    passes = sorted(d.glob("pmc_*/"), key=lambda p: int(p.name.split("_")[1]) if p.name.split("_")[1].isdigit() else 0)
+    for p in passes:
+        got = defaultdict(lambda: defaultdict(float))
+        cnt = defaultdict(lambda: defaultdict(int))
+        for f in sorted(p.glob("**/*counter_collection.csv")):
+            with open(f) as fh:
+                for r in csv.DictReader(fh):
+                    k = kernel_key(r["Kernel_Name"])
+                    if not k:
+                        continue
+                    got[k][r["Counter_Name"]] += float(r["Counter_Value"])
+                    cnt[k][r["Counter_Name"]] += 1
+        for k, cs in got.items():
+            for c, v in cs.items():
+                if c not in sums[k]:
+                    sums[k][c], n[k][c] = v, cnt[k][c]
     return sums, n
 
 
