@@ -428,3 +428,23 @@ def test_trace_frac_keeps_the_timed_launches(tmp_path):
     assert r["trace_frac"] == pytest.approx(1e6 * 10.0 / 2.2e-6 / 1e12)
     # the line's own HIP-event mean launch time (2.2 us here) prices the same: no difference
     assert r["line_events_frac"] == pytest.approx(r["trace_frac"]) and abs(r["frac_rel_diff"]) < 1e-9
+
+
+def test_c2_breakdown(tmp_path):
+    """tools/c2_breakdown.py: clock from GRBM_GUI_ACTIVE over the timed receiver dispatches, the SNR loop's share
+    of time (stamps, wave 0) and of VALU (issue model), and the loop's own fraction = line x 2.4 / clock x VALU
+    share / time share."""
+    sys.path.insert(0, str(ROOT / "tools"))
+    import c2_breakdown
+    d = tmp_path / "clock"
+    d.mkdir()
+    with open(d / "run_counter_collection.csv", "w") as f:
+        f.write("Dispatch_Id,Kernel_Name,Counter_Name,Counter_Value,Start_Timestamp,End_Timestamp\n")
+        f.write("1,\"ofdm::rx_pack_kernel<0>\",GRBM_GUI_ACTIVE,8000000,0,1000000\n")        # warm-up: 1 GHz
+        for k in range(2, 5):                                                             # timed: 2 GHz
+            f.write(f"{k},\"ofdm::rx_pack_kernel<0>\",GRBM_GUI_ACTIVE,16000000,0,1000000\n")
+    assert c2_breakdown.clock_ghz(d, 1) == pytest.approx(2.0)
+    st = tmp_path / "stamps.txt"
+    st.write_text("pack stamp wave 0: item-top barrier 5.00%; prologue work 20.00%; SNR loop 75.00%;\n"
+                  "pack stamp wave 2: item-top barrier 1.00%; prologue work 9.00%; SNR loop 90.00%;\n")
+    assert c2_breakdown.stamps(st) == {"item-top barrier": 0.05, "prologue work": 0.2, "SNR loop": 0.75}
