@@ -96,6 +96,7 @@ struct FrameArgs {
     int64_t trial0;
     int32_t q0;
     uint32_t snr_magic;
+    const float *wave_re;           // real parts of one waveform copy (nfilt floats; ensure_wave), the capture's clean part
 };
 
 // x / d and x % d for 32-bit x and d >= 1: with m = floor((2^32 - 1) / d) >= (2^32 - d) / d,
@@ -352,14 +353,16 @@ __device__ __forceinline__ float2 cfo_rot(float2 v, double f_ts, int i) {
     return make_float2(v.x * c - v.y * s, v.x * s + v.y * c);
 }
 
-// Hand-off layout: tiles of ipb items (one frame_sym_kernel block).  Within a tile, samples go in groups of
+// Hand-off: nw = 1 + n_data windows per item -- the SUM of the two rotated long training symbols (the channel
+// estimate only uses FFT(LTF1) + FFT(LTF2) = FFT(LTF1 + LTF2), OFDM.c:846-849, fft() being linear) and the n_data
+// data windows -- in tiles of ipb items (one frame_sym_kernel block).  Within a tile, samples go in groups of
 // WIN_SG: [64 / WIN_SG groups][ipb items][WIN_SG samples][nw windows] float2, so that
-//   * one item's WIN_SG x nw windows (128 B for the reference frame) are contiguous: the sync wave that owns the
-//     item writes whole 128-B lines (the earlier [64 samples][ipb items][nw] tile wrote 32-B fragments 2 KB apart,
-//     2.03x write amplification);
-//   * a symbol-kernel wave reading sample n of its lanes' windows (16 items x 4 windows for the reference frame)
-//     touches 16 lines that its reads of the group's other WIN_SG - 1 samples hit again in L1.
-constexpr int WIN_SG = 4;
+//   * one item's WIN_SG x nw slots (128 nw bytes) are contiguous: the sync wave that owns the item writes whole
+//     128-B lines for any nw (the round-3 [64 samples][ipb items][nw] tile wrote 32-B fragments 2 KB apart, 2.03x
+//     write amplification);
+//   * a symbol-kernel pass (samples 4g..4g+3 of each 16-sample group) reads 96 B of each item's 384-B group
+//     (reference frame), which the neighbouring pass reads again from L2.
+constexpr int WIN_SG = 16;
 __host__ __device__ inline float2 *win_item(float2 *win, int ipb, int nw, int64_t item) {
     const int64_t tile = item / ipb, it = item - tile * ipb;
     return win + tile * 64 * (int64_t)(ipb * nw) + it * (WIN_SG * nw);
@@ -559,10 +562,10 @@ __device__ __forceinline__ void capture_blocks(const A &a, int wave_len, float *
 #pragma unroll
         for (int u = 0; u < FRAME_CAP_U; ++u) {
             const int b = bb + 64 * u;
-            const float4 *s4 = reinterpret_cast<const float4 *>(a.wave + 4 * bm);   // bm < pb: in the waveform
-            const float4 lo = s4[0], hi = s4[1];
+            // the block's 4 clean real parts in one 16-B load (bm < pb: inside the table)
+            const float4 re = *reinterpret_cast<const float4 *>(a.wave_re + 4 * bm);
             const bool in = (uint32_t)b < nb_wave;                     // past the waveform's end: zeros
-            v[u] = in ? make_float4(lo.x, lo.z, hi.x, hi.z) : make_float4(0.f, 0.f, 0.f, 0.f);
+            v[u] = in ? re : make_float4(0.f, 0.f, 0.f, 0.f);
             bm = bm + 64 >= pb ? bm + 64 - pb : bm + 64;           // (bm + 64) mod pb (pb > 64)
         }
         if (real) {         // sigma z = sqrt(K log2 u1) (cos | sin 2 pi u2) per pair
@@ -1036,6 +1039,11 @@ __global__ __launch_bounds__(64 * W, FRAME_SYNC_MINW) void frame_sync_kernel(Fra
         // every fr[] sample the estimates read, loaded in one LDS round trip (lanes >= 16 read the coarse window
         // too, and drop it)
         const float2 cu = fr[80 + (lx & 15)], cw = fr[96 + (lx & 15)], l1 = fr[192 + lx], l2 = fr[256 + lx];
+        float2 d0 = make_float2(0.f, 0.f), d1 = d0;          // the reference frame's data windows, for the hand-off
+        if constexpr (FIX && FIX_ND == 2) {
+            d0 = fr[336 + lx];
+            d1 = fr[416 + lx];
+        }
         float2 pp = make_float2(0.f, 0.f);
         if (lx < 16) pp = make_float2(cu.x * cw.x + cu.y * cw.y, cu.y * cw.x - cu.x * cw.y);
         pp.x = wave_sum_f(pp.x);
@@ -1053,44 +1061,38 @@ __global__ __launch_bounds__(64 * W, FRAME_SYNC_MINW) void frame_sync_kernel(Fra
         // ---- coarse then fine rotation (OFDM.c:802, 825) as ONE rotation by the summed phase
         // 2 pi (fc + ff) Ts k, evaluated in fp64 revolutions (the reference's two double-precision cexp
         // products rounded to float twice; the same rotation to fp32 rounding), the result handed off
-        // directly: LTF1 [192,256), LTF2 [256,320), data d [336 + 80 d, +64) (OFDM.c:830-850, 1024-1040) ----
-        const int nw = 2 + n_data;
+        // directly: LTF1 [192,256) + LTF2 [256,320) as one window, data d [336 + 80 d, +64) (OFDM.c:830-850,
+        // 1024-1040) ----
+        const int nw = 1 + n_data;
         const int ipb = FIX ? (SYM_THREADS / 4) / ((FIX_ND + 1) / 2) : a.ipb;
         float2 *dst = win_item(a.win, ipb, nw, i);
         const double fcf_ts = (fc + ff) * TS;
-        // hand-off element j = sample j / nw of window j % nw: consecutive lanes fill the item's contiguous
-        // WIN_SG x nw slots of a sample group, 16 lanes one 128-B line for the reference frame (j / nw by a 16-bit
-        // reciprocal, exact for j < 64 nw <= 640); the dump rotates all nfr samples
-        const int nrot = dbg ? nfr : 64 * nw;
-        const uint32_t inv_nw = (65536u + (uint32_t)nw - 1u) / (uint32_t)nw;
-        if constexpr (FIX && 2 + FIX_ND == 4) {
-            // four windows: lane lx always fills window w = lx & 3 (frame sample kb + n), samples n = 16 t + lx / 4;
-            // the four fr[] reads issued together, then rotated and stored (16 lanes = one 128-B line)
-            const int w = lx & 3, kb = w < 2 ? 192 + 64 * w : 176 + 80 * w;     // 192, 256, 336, 416
-            float2 hv[4];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) hv[t] = fr[kb + 16 * t + (lx >> 2)];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const int n = 16 * t + (lx >> 2);
-                dst[win_off(n, ipb, nw) + w] = cfo_rot(hv[t], fcf_ts, kb + n);
-            }
-        } else
-        for (int j = lx; j < nrot; j += 64) {
-            int n = (int)(((uint32_t)j * inv_nw) >> 16), w = j - n * nw;
-            int k = needed_k(64 * w + n + 32);
-            if (dbg) {
-                k = j; w = -1;
-                if (k >= 192 && k < 320) {
-                    w = (k - 192) >> 6; n = (k - 192) & 63;
-                } else if (k >= 336) {
-                    const int d = (k - 336) / 80, o = k - 336 - 80 * d;
-                    if (d < n_data && o < 64) { w = 2 + d; n = o; }
+        // hand-off: window 0 = rot(LTF1) + rot(LTF2) sample by sample, windows 1 + d = data symbol d
+        if constexpr (FIX && FIX_ND == 2) {
+            // lane lx fills sample n = lx of the three windows (all four samples loaded with the CFO's): three
+            // stores, each lane's 3 slots adjacent, the item's 384-B groups whole lines once all three are done
+            const float2 u = cfo_rot(l1, fcf_ts, 192 + lx), w = cfo_rot(l2, fcf_ts, 256 + lx);
+            float2 *o = dst + win_off(lx, ipb, nw);
+            o[0] = make_float2(u.x + w.x, u.y + w.y);
+            o[1] = cfo_rot(d0, fcf_ts, 336 + lx);
+            o[2] = cfo_rot(d1, fcf_ts, 416 + lx);
+        } else {
+            if (dbg)                                           // the single-capture dump: every rotated sample
+                for (int k = lx; k < nfr; k += 64) a.dbg_frame[k] = cfo_rot(fr[k], fcf_ts, k);
+            // element j = sample j / nw of window j % nw (j / nw by a 16-bit reciprocal, exact for j < 64 nw <= 576)
+            const uint32_t inv_nw = (65536u + (uint32_t)nw - 1u) / (uint32_t)nw;
+            for (int j = lx; j < 64 * nw; j += 64) {
+                const int n = (int)(((uint32_t)j * inv_nw) >> 16), w = j - n * nw;
+                float2 v;
+                if (w == 0) {
+                    const float2 u = cfo_rot(fr[192 + n], fcf_ts, 192 + n), x = cfo_rot(fr[256 + n], fcf_ts, 256 + n);
+                    v = make_float2(u.x + x.x, u.y + x.y);
+                } else {
+                    const int k = 336 + 80 * (w - 1) + n;
+                    v = cfo_rot(fr[k], fcf_ts, k);
                 }
+                dst[win_off(n, ipb, nw) + w] = v;
             }
-            const float2 v = cfo_rot(fr[k], fcf_ts, k);
-            if (!FIX && dbg) a.dbg_frame[k] = v;
-            if (w >= 0) dst[win_off(n, ipb, nw) + w] = v;
         }
         FR_STAMP(4);                                           // coarse + fine CFO + hand-off
         if (lx == 0) {
@@ -1148,9 +1150,10 @@ __global__ __launch_bounds__(SYM_THREADS, FRAME_SYM_MINB) void frame_sym_kernel(
     const int qpi = (n_data + 1) / 2, ipb = (SYM_THREADS / 4) / qpi;   // quads per item, items per block
     const int item_l = quad / qpi, qi = quad - item_l * qpi;
     const int dsym = 2 * qi + (role & 1);
-    const int nw = 2 + n_data;
+    const int nw = 1 + n_data;
     const int dsc = min(dsym, n_data - 1);
-    const int w = role < 2 ? role : 2 + dsc;
+    // role 0: the LTF-sum window (role 1 reads the same addresses and its transform is not used); 2, 3: data
+    const int w = role < 2 ? 0 : 1 + dsc;
     for (int64_t base = (int64_t)blockIdx.x * ipb; base < a.n_items; base += (int64_t)gridDim.x * ipb) {
         const int64_t i = base + item_l;
         const bool item_ok = item_l < ipb && i < a.n_items;
@@ -1311,6 +1314,8 @@ using namespace ofdm;
         if (e_ != hipSuccess) return set_error(OFDM_E_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
     } while (0)
 
+static float *wave_re_of(Ctx *c, int len) { return (float *)((char *)c->d_wave + (size_t)len * sizeof(float2) + 64); }
+
 static int ensure_wave(Ctx *c, int conv, int payload) {
     if (conv != OFDM_CONV_C && conv != OFDM_CONV_MATLAB) return set_error(OFDM_E_ARG, "bad conv %d", conv);
     if (payload != OFDM_PAYLOAD_MESSAGE && payload != OFDM_PAYLOAD_TESTER)
@@ -1320,7 +1325,8 @@ static int ensure_wave(Ctx *c, int conv, int payload) {
     WaveArgs a{};
     a.n_data = payload_table(payload, c->message, a.table);
     const int len = wave_len_for(a.n_data);
-    int rc = c->ensure(&c->d_wave, &c->cap_wave, (size_t)len * sizeof(float2) + 64);
+    // [len] float2 waveform | power (64 B) | real parts of one copy (len / FR_REPS floats, 16-B aligned)
+    int rc = c->ensure(&c->d_wave, &c->cap_wave, (size_t)len * sizeof(float2) + 64 + (size_t)len / FR_REPS * sizeof(float));
     if (rc) return rc;
     a.wave = (float2 *)c->d_wave;
     a.power = (double *)((char *)c->d_wave + (size_t)len * sizeof(float2));
@@ -1329,6 +1335,9 @@ static int ensure_wave(Ctx *c, int conv, int payload) {
     if (conv == OFDM_CONV_C) hipLaunchKernelGGL(frame_wave_kernel<OFDM_CONV_C>, dim3(1), dim3(256), 0, c->stream, a);
     else hipLaunchKernelGGL(frame_wave_kernel<OFDM_CONV_MATLAB>, dim3(1), dim3(256), 0, c->stream, a);
     HIPOK(hipGetLastError());
+    // the capture's clean real parts, dense (the sync kernel loads 4 per 16 B instead of 4 complex samples per 32 B)
+    HIPOK(hipMemcpy2DAsync(wave_re_of(c, len), sizeof(float), c->d_wave, sizeof(float2), sizeof(float),
+                           (size_t)len / FR_REPS, hipMemcpyDeviceToDevice, c->stream));
     HIPOK(hipMemcpyAsync(&c->wave_power, a.power, sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIPOK(hipStreamSynchronize(c->stream));
     c->wave_key = key;
@@ -1351,6 +1360,7 @@ static int check_opts(const Ctx *c, const ofdm_rx_opts *o) {
 
 static void fill_frame_args(FrameArgs &a, Ctx *c, const ofdm_rx_opts *o, int noise, uint64_t seed, int payload) {
     a.wave = (const float2 *)c->d_wave;
+    a.wave_re = wave_re_of(c, c->wave_len);
     a.cap_len = capture_len(c, o);
     a.float_cfo = o->float_cfo;
     a.matlab = o->matlab_slicer;
@@ -1383,13 +1393,13 @@ constexpr int64_t FRAME_CHUNK_ITEMS = int64_t(1) << FRAME_CHUNK_LOG2;
 // items per chunk for n_data data symbols: 2^22, capped so that the hand-off buffer holds no more windows than the
 // reference message's 2^22 items do (8 GiB; ADVICE r3: 8-symbol messages would otherwise take 21 GB)
 static int64_t frame_chunk_items(int n_data) {
-    return std::min<int64_t>(FRAME_CHUNK_ITEMS, FRAME_CHUNK_ITEMS * 4 / (2 + n_data));
+    return std::min<int64_t>(FRAME_CHUNK_ITEMS, FRAME_CHUNK_ITEMS * 3 / (1 + n_data));
 }
 constexpr int64_t FRAME_CHUNK_MIN = int64_t(1) << 16;    // halving stops here when the buffer cannot be allocated
 
 // K4b then K4b' over a.n_items items starting at a.item0, through the context's hand-off buffer
 static int run_frame_chunk(Ctx *c, FrameArgs &a) {
-    const int nw = 2 + a.n_data;
+    const int nw = 1 + a.n_data;
     if (a.n_snr < 1 || a.n_items < 0 || a.n_items + a.n_snr + FRAME_ITEM_RUN > (int64_t(1) << 31))
         return set_error(OFDM_E_ARG, "frame chunk: items or SNR points out of range");
     a.trial0 = a.item0 / a.n_snr;

@@ -30,7 +30,6 @@ __device__ __forceinline__ float dpp_f(float v) {
 template <int CTRL>
 __device__ __forceinline__ float2 dpp_c(float2 v) { return make_float2(dpp_f<CTRL>(v.x), dpp_f<CTRL>(v.y)); }
 constexpr int DPP_QUAD_BCAST0 = 0x00;   // quad_perm [0,0,0,0]
-constexpr int DPP_QUAD_BCAST1 = 0x55;   // quad_perm [1,1,1,1]
 
 __device__ __forceinline__ void channel_taps(uint32_t f_lo, uint32_t f_hi, uint32_t k0, uint32_t k1, float2 (&h)[4]) {
     const Gauss4 a = gauss4(f_lo, f_hi, 0u, STREAM_CHAN, k0, k1);
@@ -181,18 +180,12 @@ __device__ __forceinline__ void demap_sub(const float2 (&x)[64], uint32_t t, HF 
     st.be += __popc(em & 0x55555555u) + __popc((em ^ (em >> 1)) & 0x55555555u);
 }
 
-// dpp(a) + b as one v_add_f32_dpp (bound_ctrl lets the DPP combiner fold the move)
-template <int CTRL>
-__device__ __forceinline__ float dpp_add(float a, float b) {
-    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(a), CTRL, 0xF, 0xF, true)) + b;
-}
-
-// LTF least-squares equaliser for a quad {LTF1, LTF2, D0, D1} of one frame: S = F1 + F2 from
-// lanes 0 and 1, H = 0.5 Lf S (OFDM.c:846-849), Z = Y / H = 2 Lf Y conj(S) / |S|^2 (OFDM.c:1044-1052).
+// LTF least-squares equaliser for a quad {LTF1 + LTF2, -, D0, D1} of one frame (frame_sym_kernel): the LTF pair
+// arrives as one window, so lane 0's spectrum is S = FFT(LTF1 + LTF2) = F1 + F2 (fft() is linear), H = 0.5 Lf S
+// (OFDM.c:846-849), Z = Y / H = 2 Lf Y conj(S) / |S|^2 (OFDM.c:1044-1052).
 template <int BIN>
 __device__ __forceinline__ EqOut<2> ls_equalise(float2 Y) {
-    const float2 F2 = dpp_c<DPP_QUAD_BCAST1>(Y);
-    const float2 S = make_float2(dpp_add<DPP_QUAD_BCAST0>(Y.x, F2.x), dpp_add<DPP_QUAD_BCAST0>(Y.y, F2.y));
+    const float2 S = dpp_c<DPP_QUAD_BCAST0>(Y);
     EqOut<2> e;
     e.r = __builtin_amdgcn_rcpf(fmaf(S.x, S.x, S.y * S.y));
     e.u = cscale(cmulc(Y, S), (float)ltf_sign(BIN));
