@@ -355,13 +355,13 @@ __device__ __forceinline__ float2 cfo_rot(float2 v, double f_ts, int i) {
 
 // Hand-off: nw = 1 + n_data windows per item -- the SUM of the two rotated long training symbols (the channel
 // estimate only uses FFT(LTF1) + FFT(LTF2) = FFT(LTF1 + LTF2), OFDM.c:846-849, fft() being linear) and the n_data
-// data windows -- in tiles of ipb items (one frame_sym_kernel block).  Within a tile, samples go in groups of
-// WIN_SG: [64 / WIN_SG groups][ipb items][WIN_SG samples][nw windows] float2, so that
-//   * one item's WIN_SG x nw slots (128 nw bytes) are contiguous: the sync wave that owns the item writes whole
-//     128-B lines for any nw (the round-3 [64 samples][ipb items][nw] tile wrote 32-B fragments 2 KB apart, 2.03x
-//     write amplification);
-//   * a symbol-kernel pass (samples 4g..4g+3 of each 16-sample group) reads 96 B of each item's 384-B group
-//     (reference frame), which the neighbouring pass reads again from L2.
+// data windows -- in tiles of ipb items (one frame_sym_kernel block).  Sample n = 16 q + r of a window sits at
+// position p = 4 r + q, and a tile holds [4 groups][ipb items][16 positions][nw windows] float2, so that
+//   * group g holds samples {16 q + r : 4 g <= r < 4 g + 4, q < 4}: exactly the 16 samples the symbol kernel's
+//     load pass g reads (its first radix-4 stage combines x[n], x[n + 16], x[n + 32], x[n + 48]), as one run of
+//     16 nw slots (128 nw bytes, whole 128-B lines) per item;
+//   * the sync wave that owns the item writes those whole lines (the round-3 [64 samples][ipb items][nw] tile
+//     wrote 32-B fragments 2 KB apart, 2.03x write amplification).
 constexpr int WIN_SG = 16;
 __host__ __device__ inline float2 *win_item(float2 *win, int ipb, int nw, int64_t item) {
     const int64_t tile = item / ipb, it = item - tile * ipb;
@@ -369,7 +369,8 @@ __host__ __device__ inline float2 *win_item(float2 *win, int ipb, int nw, int64_
 }
 // offset of sample n of window 0 from win_item()
 __host__ __device__ inline int win_off(int n, int ipb, int nw) {
-    return (n / WIN_SG) * (ipb * WIN_SG * nw) + (n % WIN_SG) * nw;
+    const int p = ((n & 15) << 2) | (n >> 4);
+    return (p / WIN_SG) * (ipb * WIN_SG * nw) + (p % WIN_SG) * nw;
 }
 
 // j-th frame sample the receiver reads (j < 160 + 64 nd): the coarse-CFO lag window [80, 112)
@@ -1070,7 +1071,7 @@ __global__ __launch_bounds__(64 * W, FRAME_SYNC_MINW) void frame_sync_kernel(Fra
         // hand-off: window 0 = rot(LTF1) + rot(LTF2) sample by sample, windows 1 + d = data symbol d
         if constexpr (FIX && FIX_ND == 2) {
             // lane lx fills sample n = lx of the three windows (all four samples loaded with the CFO's): three
-            // stores, each lane's 3 slots adjacent, the item's 384-B groups whole lines once all three are done
+            // stores, each lane's 3 slots adjacent, the item's four 384-B groups whole lines once all three are done
             const float2 u = cfo_rot(l1, fcf_ts, 192 + lx), w = cfo_rot(l2, fcf_ts, 256 + lx);
             float2 *o = dst + win_off(lx, ipb, nw);
             o[0] = make_float2(u.x + w.x, u.y + w.y);
