@@ -1161,7 +1161,11 @@ __global__ __launch_bounds__(SYM_THREADS, FRAME_SYM_MINB) void frame_sym_kernel(
         const bool dlane = item_ok && role >= 2 && dsym < n_data;
         const float2 *src = win_item(a.win, ipb, nw, item_ok ? i : base) + w;
         float2 x[64];
-        // load fused with the first radix-4 stage, 16 samples at a time (fft() = DFT(x (-1)^n))
+#ifndef FRAME_SYM_GROUPS
+#define FRAME_SYM_GROUPS 1      // hand-off groups loaded per batch of first radix-4 stages (A/B: 1, 2, 4)
+#endif
+        // load fused with the first radix-4 stage, FRAME_SYM_GROUPS x 16 samples (hand-off groups) at a time
+        // (fft() = DFT(x (-1)^n))
         static_for<0, 4>([&](auto gc) {
             constexpr int g = decltype(gc)::value;
             gcf2 *sp = (gcf2 *)src;
@@ -1171,8 +1175,12 @@ __global__ __launch_bounds__(SYM_THREADS, FRAME_SYM_MINB) void frame_sym_kernel(
                 const float2 v = gld(sp, win_off(n, ipb, nw));
                 x[n] = (n & 1) ? make_float2(-v.x, -v.y) : v;
             });
-            static_for<0, 4>([&](auto ic) { dif_stage1<false, 4 * g + decltype(ic)::value>(x); });
-            sched_fence();
+            if constexpr ((g + 1) % FRAME_SYM_GROUPS == 0) {
+                static_for<0, 4 * FRAME_SYM_GROUPS>([&](auto ic) {
+                    dif_stage1<false, 4 * (g + 1 - FRAME_SYM_GROUPS) + decltype(ic)::value>(x);
+                });
+                sched_fence();
+            }
         });
         const uint32_t wd[4] = {a.dtable[4 * dsc], a.dtable[4 * dsc + 1], a.dtable[4 * dsc + 2], a.dtable[4 * dsc + 3]};
         SymState st;
