@@ -1162,7 +1162,8 @@ __global__ __launch_bounds__(SYM_THREADS, FRAME_SYM_MINB) void frame_sym_kernel(
         const float2 *src = win_item(a.win, ipb, nw, item_ok ? i : base) + w;
         float2 x[64];
 #ifndef FRAME_SYM_GROUPS
-#define FRAME_SYM_GROUPS 1      // hand-off groups loaded per batch of first radix-4 stages (A/B: 1, 2, 4)
+#define FRAME_SYM_GROUPS 2      // hand-off groups loaded per batch of first radix-4 stages (A/B: 2 +0.4 % over 1; 4
+                                // needs 172 VGPRs, 2 waves/SIMD, and gains nothing; profiles/r04/ab/x_ab_groups.txt)
 #endif
         // load fused with the first radix-4 stage, FRAME_SYM_GROUPS x 16 samples (hand-off groups) at a time
         // (fft() = DFT(x (-1)^n))
