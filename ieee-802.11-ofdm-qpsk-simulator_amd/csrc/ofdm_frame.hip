@@ -1074,9 +1074,21 @@ __global__ __launch_bounds__(64 * W, FRAME_SYNC_MINW) void frame_sync_kernel(Fra
             // stores, each lane's 3 slots adjacent, the item's four 384-B groups whole lines once all three are done
             const float2 u = cfo_rot(l1, fcf_ts, 192 + lx), w = cfo_rot(l2, fcf_ts, 256 + lx);
             float2 *o = dst + win_off(lx, ipb, nw);
-            o[0] = make_float2(u.x + w.x, u.y + w.y);
-            o[1] = cfo_rot(d0, fcf_ts, 336 + lx);
-            o[2] = cfo_rot(d1, fcf_ts, 416 + lx);
+#ifndef FRAME_HANDOFF_NT
+#define FRAME_HANDOFF_NT 0      // A/B: non-temporal hand-off stores (read back by the symbol kernel from HBM anyway)
+#endif
+            if constexpr (FRAME_HANDOFF_NT) {
+                auto nt = [](float2 *q, float2 v) {
+                    __builtin_nontemporal_store(__builtin_bit_cast(unsigned long long, v), (unsigned long long *)q);
+                };
+                nt(o, make_float2(u.x + w.x, u.y + w.y));
+                nt(o + 1, cfo_rot(d0, fcf_ts, 336 + lx));
+                nt(o + 2, cfo_rot(d1, fcf_ts, 416 + lx));
+            } else {
+                o[0] = make_float2(u.x + w.x, u.y + w.y);
+                o[1] = cfo_rot(d0, fcf_ts, 336 + lx);
+                o[2] = cfo_rot(d1, fcf_ts, 416 + lx);
+            }
         } else {
             if (dbg)                                           // the single-capture dump: every rotated sample
                 for (int k = lx; k < nfr; k += 64) a.dbg_frame[k] = cfo_rot(fr[k], fcf_ts, k);
