@@ -564,7 +564,11 @@ __device__ __forceinline__ void capture_blocks(const A &a, int wave_len, float *
         for (int u = 0; u < FRAME_CAP_U; ++u) {
             const int b = bb + 64 * u;
             // the block's 4 clean real parts in one 16-B load (bm < pb: inside the table)
-            const float4 re = *reinterpret_cast<const float4 *>(a.wave_re + 4 * bm);
+            float4 re = *reinterpret_cast<const float4 *>(a.wave_re + 4 * bm);
+#ifndef FRAME_CAP_ULOAD
+#define FRAME_CAP_ULOAD 0       // A/B: the table loads issued by every lane (no exec-masked branch per block)
+#endif
+            if constexpr (FRAME_CAP_ULOAD) asm volatile("" : "+v"(re.x), "+v"(re.y), "+v"(re.z), "+v"(re.w));
             const bool in = (uint32_t)b < nb_wave;                     // past the waveform's end: zeros
             v[u] = in ? re : make_float4(0.f, 0.f, 0.f, 0.f);
             bm = bm + 64 >= pb ? bm + 64 - pb : bm + 64;           // (bm + 64) mod pb (pb > 64)
