@@ -563,12 +563,9 @@ __device__ __forceinline__ void capture_blocks(const A &a, int wave_len, float *
 #pragma unroll
         for (int u = 0; u < FRAME_CAP_U; ++u) {
             const int b = bb + 64 * u;
-            // the block's 4 clean real parts in one 16-B load (bm < pb: inside the table)
-            float4 re = *reinterpret_cast<const float4 *>(a.wave_re + 4 * bm);
-#ifndef FRAME_CAP_ULOAD
-#define FRAME_CAP_ULOAD 0       // A/B: the table loads issued by every lane (no exec-masked branch per block)
-#endif
-            if constexpr (FRAME_CAP_ULOAD) asm volatile("" : "+v"(re.x), "+v"(re.y), "+v"(re.z), "+v"(re.w));
+            // the block's 4 clean real parts in one 16-B load (bm < pb: inside the table; the compiler keeps it under
+            // `in`, and forcing it on every lane measured 1 % slower, profiles/r04/ab/ab_ab_ntu.txt)
+            const float4 re = *reinterpret_cast<const float4 *>(a.wave_re + 4 * bm);
             const bool in = (uint32_t)b < nb_wave;                     // past the waveform's end: zeros
             v[u] = in ? re : make_float4(0.f, 0.f, 0.f, 0.f);
             bm = bm + 64 >= pb ? bm + 64 - pb : bm + 64;           // (bm + 64) mod pb (pb > 64)
@@ -764,11 +761,9 @@ __global__ __launch_bounds__(64 * W, FRAME_SYNC_MINW) void frame_sync_kernel(Fra
                 // immediate offset (< 1 KB) -- otherwise the compiler folds part of the table base into constants
                 // too large for the offset field and spends one v_add per read on addresses
                 using LdsF = const __attribute__((address_space(3))) float;
-#ifndef FRAME_EXP_NOWRAP
+                // (the period wrap puts part of a 32-lane group on a shifted bank pattern; a timing-only build without
+                // it measured no difference and 19 of 527 conflict cycles per item, profiles/r04/pmc_ab/q_lds_nowrap)
                 LdsF *ti_ = (LdsF *)(imt + im_mod(im0 + n0));
-#else           // A/B timing only (wrong imaginary parts): table reads without the period wrap's bank shift
-                LdsF *ti_ = (LdsF *)(imt + ((im0 + n0) & 1023));
-#endif
                 LdsF *tr_ = (LdsF *)(r + n0);
                 opaque(ti_);
                 opaque(tr_);
@@ -1077,22 +1072,11 @@ __global__ __launch_bounds__(64 * W, FRAME_SYNC_MINW) void frame_sync_kernel(Fra
             // lane lx fills sample n = lx of the three windows (all four samples loaded with the CFO's): three
             // stores, each lane's 3 slots adjacent, the item's four 384-B groups whole lines once all three are done
             const float2 u = cfo_rot(l1, fcf_ts, 192 + lx), w = cfo_rot(l2, fcf_ts, 256 + lx);
+            // (non-temporal stores measured neutral, profiles/r04/ab/aa_ab_nt.txt)
             float2 *o = dst + win_off(lx, ipb, nw);
-#ifndef FRAME_HANDOFF_NT
-#define FRAME_HANDOFF_NT 0      // A/B: non-temporal hand-off stores (read back by the symbol kernel from HBM anyway)
-#endif
-            if constexpr (FRAME_HANDOFF_NT) {
-                auto nt = [](float2 *q, float2 v) {
-                    __builtin_nontemporal_store(__builtin_bit_cast(unsigned long long, v), (unsigned long long *)q);
-                };
-                nt(o, make_float2(u.x + w.x, u.y + w.y));
-                nt(o + 1, cfo_rot(d0, fcf_ts, 336 + lx));
-                nt(o + 2, cfo_rot(d1, fcf_ts, 416 + lx));
-            } else {
-                o[0] = make_float2(u.x + w.x, u.y + w.y);
-                o[1] = cfo_rot(d0, fcf_ts, 336 + lx);
-                o[2] = cfo_rot(d1, fcf_ts, 416 + lx);
-            }
+            o[0] = make_float2(u.x + w.x, u.y + w.y);
+            o[1] = cfo_rot(d0, fcf_ts, 336 + lx);
+            o[2] = cfo_rot(d1, fcf_ts, 416 + lx);
         } else {
             if (dbg)                                           // the single-capture dump: every rotated sample
                 for (int k = lx; k < nfr; k += 64) a.dbg_frame[k] = cfo_rot(fr[k], fcf_ts, k);
