@@ -1446,7 +1446,8 @@ static int run_frame_chunk(Ctx *c, FrameArgs &a) {
     // Long captures (8-symbol messages: 24 KB per wave) could run one-wave blocks, which fit five per CU where
     // one four-wave block fits; but five waves on four SIMDs leave three SIMDs with one wave each, and
     // the 8-symbol sweep measured 4.07e8 with one-wave blocks against 4.16e8 with four-wave ones (round 4,
-    // profiles/r04/ab/h_frame8*.json).  So one-wave blocks run only when they give every SIMD more waves:
+    // profiles/r04/ab/h_frame8*.json; after the real-part table 4.28e8 against 4.50e8, and 4.15e8 with two-wave
+    // blocks, ae_frame8_blocks.txt).  So one-wave blocks run only when they give every SIMD more waves:
     // resident = whole waves per SIMD x 4, from W x floor(LDS per CU / block LDS), at most 12
     const size_t lds1 = frame_lds_bytes(a.cap_len, a.n_data, a.n_snr, a.imt_len, a.word_stats, 1) + FRAME_LDS_PAD;
     auto resident = [](size_t b, int w) {
@@ -1454,19 +1455,13 @@ static int run_frame_chunk(Ctx *c, FrameArgs &a) {
     };
     const bool one = !fixed && ((resident(lds1, 1) > resident(lds, SYNC_WAVES) && !getenv("OFDM_FRAME_BLOCK4")) ||
                                 getenv("OFDM_FRAME_BLOCK1"));
-    // A/B: two-wave blocks for long captures (OFDM_FRAME_BLOCK2)
-    const bool two = !fixed && !one && getenv("OFDM_FRAME_BLOCK2");
-    const size_t lds2 = frame_lds_bytes(a.cap_len, a.n_data, a.n_snr, a.imt_len, a.word_stats, 2) + FRAME_LDS_PAD;
     const void *ks = fixed ? frame_fix_kernel()
                    : one   ? reinterpret_cast<const void *>(&frame_sync_kernel<0, 0, 1>)
-                   : two   ? reinterpret_cast<const void *>(&frame_sync_kernel<0, 0, 2>)
                            : reinterpret_cast<const void *>(&frame_sync_kernel<0, 0>);
-    const int waves = one ? 1 : two ? 2 : SYNC_WAVES;
-    const size_t lds_k = one ? lds1 : two ? lds2 : lds;
-    const dim3 gs(occupancy_grid(ks, 64 * waves, lds_k, c->cus, (runs + waves - 1) / waves, 1));
+    const int waves = one ? 1 : SYNC_WAVES;
+    const dim3 gs(occupancy_grid(ks, 64 * waves, one ? lds1 : lds, c->cus, (runs + waves - 1) / waves, 1));
     if (fixed) launch_frame_fix(c->stream, a, gs, lds);
     else if (one) hipLaunchKernelGGL((frame_sync_kernel<0, 0, 1>), gs, dim3(64), lds1, c->stream, a);
-    else if (two) hipLaunchKernelGGL((frame_sync_kernel<0, 0, 2>), gs, dim3(128), lds2, c->stream, a);
     else hipLaunchKernelGGL((frame_sync_kernel<0, 0>), gs, dim3(SYNC_THREADS), lds, c->stream, a);
     launch_frame_sym(c->stream, a, c->cus);
     HIPOK(hipGetLastError());
