@@ -434,21 +434,16 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
             // LS AWGN: wave 2 warms L2 with the next item's rows at the start of its last SNR iteration, one
             // iteration before the next prologue reads them (warmed in the prologue, a whole item earlier, most
             // lines were evicted again: 64 blocks per XCD warm 4 MB into its 4 MB L2)
-#ifndef PACK_WARM_SPREAD
-#define PACK_WARM_SPREAD 0      // A/B: the late warm-up's 8 loads per lane spread over the 4 waves (2 each)
-#endif
             if constexpr (WLATE) {
-                if ((PACK_WARM_SPREAD || wv == 2) && q + 4 * ns >= a.n_snr) {
+                if (wv == 2 && q + 4 * ns >= a.n_snr) {
                     const int nx = __builtin_amdgcn_readfirstlane(next_item);
                     using KArgsW = const __attribute__((address_space(4))) RxArgs;
                     KArgsW *apw = (KArgsW *)__builtin_amdgcn_kernarg_segment_ptr();
                     if (nx < n_items && apw->own.n_sym == 0) {
                         const int64_t ng = nx < R * B ? nx : R * B + (nx - R * B) / S;
                         const int ln = SPLIT ? lane_fresh() : lane;     // split: nothing lane-derived held
-                        constexpr int NW = PACK_WARM_SPREAD ? 2 : 8;
 #pragma unroll
-                        for (int ii = 0; ii < NW; ++ii) {
-                            const int i = PACK_WARM_SPREAD ? 2 * wv + ii : ii;
+                        for (int i = 0; i < 8; ++i) {
                             const int line = ln + 64 * i;                      // 0..511
                             const float2 *p = a.tx + (int64_t)(16 + (line >> 3)) * a.pitch + ng * PK_SYMS + (line & 7) * 16;
                             __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)p,
