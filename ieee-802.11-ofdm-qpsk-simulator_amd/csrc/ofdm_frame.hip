@@ -1173,16 +1173,7 @@ __global__ __launch_bounds__(SYM_THREADS, FRAME_SYM_MINB) void frame_sym_kernel(
             opaque(sp);
             static_for<0, 16>([&](auto pc) {
                 constexpr int n = 16 * (decltype(pc)::value >> 2) + 4 * g + (decltype(pc)::value & 3);
-#ifndef FRAME_SYM_NT
-#define FRAME_SYM_NT 0          // A/B: non-temporal hand-off loads (each byte is read once)
-#endif
-                float2 v;
-                if constexpr (FRAME_SYM_NT) {
-                    const f2v t = __builtin_nontemporal_load(sp + win_off(n, ipb, nw));
-                    v = make_float2(t.x, t.y);
-                } else {
-                    v = gld(sp, win_off(n, ipb, nw));
-                }
+                const float2 v = gld(sp, win_off(n, ipb, nw));
                 x[n] = (n & 1) ? make_float2(-v.x, -v.y) : v;
             });
             if constexpr ((g + 1) % FRAME_SYM_GROUPS == 0) {
