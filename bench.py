@@ -42,7 +42,9 @@ BYTES_PER_SYMBOL_SNR = 652     # 80 x 8 B clean symbol + 12 B pac
 # wave64 VALU issue peak: 256 CUs x 4 SIMDs x 1 wave-instruction per 2 cycles at 2.4 GHz
 # (MI355X_MICROARCH.md "Wave scheduling"; tools/ubench_valu.hip)
 VALU_PEAK_PER_S = 256 * 4 * 0.5 * 2.4e9
-FRAME_CAPTURE_BYTES = 3008 * 8     # capture samples read per trial (L2-resident 78 KB waveform)
+# capture samples read per trial (complex f32, from the L2-resident waveform): 3008 for the reference message,
+# int(0.307 x 19400) = 5955 for frame8's 8-symbol waveform (OFDM.c:945)
+FRAME_CAPTURE_SAMPLES = {"frame": 3008, "frame8": 5955}
 SNR_GRID = np.arange(0.0, 31.0, 2.0)
 MAX_CHUNK_FRAMES = 1 << 23         # largest device-resident Tx batch (16.8M symbols, 10.7 GB of HBM)
 PIPE_CHUNKS = 4                    # Tx / receiver pipeline depth of a step (symbol workloads)
@@ -408,7 +410,10 @@ def main():
     eng = pkg.Engine(dev)
     frame_mode = args.workload.startswith("frame")
     if args.workload == "frame8":
-        assert eng.set_message(FRAME8_MESSAGE) == 8
+        # not inside an assert: under python -O the message would silently stay the 2-symbol reference one
+        got = eng.set_message(FRAME8_MESSAGE)
+        if got != dpf:
+            raise SystemExit(f"frame8: set_message framed {got} data symbols, expected {dpf}")
     counters = eng.new_counters(len(SNR_GRID))
     chunks = plan_chunks(first, frames, args.chunks)
     # real-noise sweeps on the packed receivers (c2, c3, c4, c5): every Tx batch built inside the receivers
@@ -458,7 +463,7 @@ def main():
     value = total_units / elapsed
     rx_avg_s = rx_ms / max(rx_n, 1) / 1e3
     units_per_launch = frames * dpf * n_snr * args.steps / max(rx_n, 1)  # this rank's units per receiver launch
-    bytes_per_unit = FRAME_CAPTURE_BYTES / 2 if frame_mode else BYTES_PER_SYMBOL_SNR
+    bytes_per_unit = FRAME_CAPTURE_SAMPLES[args.workload] * 8 / dpf if frame_mode else BYTES_PER_SYMBOL_SNR
     res = pkg.SweepResult(SNR_GRID, c)
     pmc = load_pmc(args.workload)
     # the receiver kernel this workload launches (ofdm_symbol.hip launch_rx): real-noise AWGN sweeps and
@@ -470,7 +475,6 @@ def main():
     lib_id = codeobj.workload_build_id(abi.library_file(), args.workload)
     roofline, traffic = make_roofline(pmc, lib_id, kernel, args.workload, units_per_launch, rx_avg_s, rx_n,
                                       fused and not frame_mode)
-    hbm_alg = units_per_launch * bytes_per_unit / rx_avg_s / 1e9
     if rank == 0:
         line = {
             "metric": "OFDM symbols/sec (whole node) over BER-vs-SNR sweep; achieved HBM GB/s vs peak",
@@ -495,14 +499,17 @@ def main():
             # the binding roofline: VALU issue (make_roofline)
             "roofline": roofline,
             # HBM: the measured traffic (PMC) against the HBM peak is the HBM roofline fraction.  SURVEY
-            # §8(d)'s streaming figure (652 B per unit, as if each symbol were re-read per SNR point) is kept
-            # as a rate only: the kernels stage a symbol once per launch, so it is not traffic and has no
-            # fraction of the peak
+            # §8(d)'s streaming figure (652 B per unit, as if each symbol were re-read per SNR point) is NOT
+            # traffic: the kernels stage a symbol once per launch for all SNR points.  Only its per-unit size is
+            # kept, with no rate, so that no field of the line reads as a bandwidth above the HBM peak
             "hbm": {"measured_bytes_per_launch": traffic,
                     "measured_gbs": traffic / rx_avg_s / 1e9 if traffic else None,
                     "measured_frac": traffic / rx_avg_s / 1e9 / HBM_PEAK_GBS if traffic else None,
                     "peak_gbs": HBM_PEAK_GBS,
-                    "streaming_equivalent": {"bytes_per_unit": bytes_per_unit, "gbs": hbm_alg}},
+                    "survey_streaming_bytes_per_unit": {
+                        "bytes_per_unit": bytes_per_unit, "is_traffic": False,
+                        "note": "SURVEY 8(d) per-unit size if every unit were streamed from HBM; the fused "
+                                "kernels read each symbol once per launch (see measured_bytes_per_launch)"}},
             "kernels_ms": {"rx_total": rx_ms, "rx_launches": rx_n, "tx_total": tx_ms, "tx_launches": tx_n},
             "results": {"ber": res.ber.tolist(), "evm_pre_db": res.evm_pre_db.tolist(),
                         "frames_per_snr": int(c[0, abi.C_FRAMES])},

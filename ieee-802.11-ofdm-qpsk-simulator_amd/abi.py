@@ -42,6 +42,8 @@ _SIGS = {
     "ofdm_ctx_destroy": (C.c_int, [_V]),
     "ofdm_ctx_set_stream": (C.c_int, [_V, _V]),
     "ofdm_ctx_synchronize": (C.c_int, [_V]),
+    "ofdm_ctx_trim": (C.c_int, [_V, C.POINTER(C.c_int64)]),
+    "ofdm_ctx_scratch_bytes": (C.c_int, [_V, C.POINTER(C.c_int64)]),
     "ofdm_timing_enable": (C.c_int, [_V, C.c_int]),
     "ofdm_timing_query": (C.c_int, [_V, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     "ofdm_timing_reset": (C.c_int, [_V]),

@@ -3,6 +3,8 @@
 // ofdm_symbol.hip / ofdm_frame.hip).
 #include <hip/hip_runtime.h>
 #include <cmath>
+#include <cstdint>
+#include <cstdlib>
 #include <complex>
 #include <cstdio>
 #include <cstring>
@@ -110,11 +112,19 @@ void Ctx::resolve() {
     done.clear();
 }
 
+// OFDM_DEVICE_ALLOC_CAP=<bytes>: a scratch allocation above it fails as if hipMalloc had (OFDM_E_NOMEM) -- the
+// test hook of the frame sweep's chunk-halving path (tests/test_gpu_frame.py::test_frame_sweep_nomem_halving_*)
+static size_t alloc_cap() {
+    const char *s = getenv("OFDM_DEVICE_ALLOC_CAP");
+    return s && *s ? (size_t)strtoull(s, nullptr, 10) : SIZE_MAX;
+}
+
 int Ctx::ensure(void **p, size_t *cap, size_t bytes) {
     if (*cap >= bytes) return OFDM_OK;
     if (*p) hipFree(*p);
     *p = nullptr;
     *cap = 0;
+    if (bytes > alloc_cap()) return set_error(OFDM_E_NOMEM, "allocation of %zu bytes above OFDM_DEVICE_ALLOC_CAP", bytes);
     if (hipMalloc(p, bytes) != hipSuccess) {
         *p = nullptr;
         return set_error(OFDM_E_NOMEM, "hipMalloc(%zu) failed", bytes);
@@ -202,6 +212,36 @@ int ofdm_ctx_destroy(ofdm_ctx *ctx) {
     if (c->tx_stream) hipStreamDestroy(c->tx_stream);
     if (c->own) hipStreamDestroy(c->own);
     delete c;
+    return OFDM_OK;
+}
+
+int ofdm_ctx_trim(ofdm_ctx *ctx, int64_t *released) {
+    Ctx *c = reinterpret_cast<Ctx *>(ctx);
+    if (!c) return set_error(OFDM_E_ARG, "ctx is NULL");
+    HIPOK(hipSetDevice(c->device));
+    // every launch that may still read or write the scratch has finished (both of the context's streams)
+    HIPOK(hipStreamSynchronize(c->stream));
+    if (c->tx_stream) HIPOK(hipStreamSynchronize(c->tx_stream));
+    int64_t n = 0;
+    struct { void **p; size_t *cap; } bufs[] = {{&c->d_tx, &c->cap_tx}, {&c->d_bits, &c->cap_bits}, {&c->d_tx2, &c->cap_tx2},
+                                                {&c->d_bits2, &c->cap_bits2}, {&c->d_cnt, &c->cap_cnt},
+                                                {&c->d_scratch, &c->cap_scratch}, {&c->d_scratch2, &c->cap_scratch2}};
+    for (auto &b : bufs) {
+        if (*b.p) {
+            HIPOK(hipFree(*b.p));
+            n += (int64_t)*b.cap;
+        }
+        *b.p = nullptr;
+        *b.cap = 0;
+    }
+    if (released) *released = n;
+    return OFDM_OK;
+}
+
+int ofdm_ctx_scratch_bytes(ofdm_ctx *ctx, int64_t *bytes) {
+    Ctx *c = reinterpret_cast<Ctx *>(ctx);
+    if (!c || !bytes) return set_error(OFDM_E_ARG, "bad scratch_bytes arguments");
+    *bytes = (int64_t)(c->cap_tx + c->cap_bits + c->cap_tx2 + c->cap_bits2 + c->cap_cnt + c->cap_scratch + c->cap_scratch2);
     return OFDM_OK;
 }
 

@@ -351,6 +351,40 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
     return t;
 }
 
+// ------------------------------------------------------------------ atan2 for the CFO estimates
+// atan2f (OFDM.c:798, 821) as the device library's (OCML) atan2f computes it for FINITE arguments, without its
+// frexp / ldexp scaling of the quotient and its inf / NaN paths: min(|x|,|y|) * rcp(max) is the library's scaled
+// quotient bit for bit for normal arguments (rcp of a power-of-two-scaled mantissa scales exactly), followed by
+// the same minimax polynomial and quadrant fix-ups -- the same result bit for bit wherever it is a normal float
+// (when |y / x| < 2^-126 the subnormal quotient may round one subnormal step apart).  Arguments whose larger
+// magnitude lies outside [2^-64, 2^64] (subnormals included) are first scaled by 2^64 or 2^-64 (exact), so rcp
+// never sees a subnormal (rcp = inf, and 0 * inf would be a NaN phase) nor returns one (flushed: atan2(m, m) = 0
+// instead of pi/4 for m > 2^126).  Signed zeros as atan2f: (+-0, +0) -> +-0,
+// (+-0, -0) -> +-pi, (y, +-0) -> +-pi/2.  Infinite or NaN arguments are outside the contract (a CFO correlation
+// sum is finite).  tests/device/atan2_check.hip compares it with atan2f on the GPU (tests/test_gpu_device.py).
+__device__ __forceinline__ float atan2_cfo(float y, float x) {
+    float ax = fabsf(x), ay = fabsf(y);
+    const float m = fmaxf(ax, ay);
+    const float sc = m < 0x1p-64f ? 0x1p64f : m > 0x1p64f ? 0x1p-64f : 1.0f;    // exact power-of-two scaling
+    ax *= sc;
+    ay *= sc;
+    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+    float a = mn * __builtin_amdgcn_rcpf(mx);
+    a = mn > 0.f ? a : 0.f;                                        // 0 / 0 and 0 / m: 0
+    const float s = a * a;
+    float t = fmaf(s, __uint_as_float(0x3b2d2a58u), __uint_as_float(0xbc7a590cu));
+    t = fmaf(s, t, __uint_as_float(0x3d29fb3fu));
+    t = fmaf(s, t, __uint_as_float(0xbd97d4d7u));
+    t = fmaf(s, t, __uint_as_float(0x3dd931b2u));
+    t = fmaf(s, t, __uint_as_float(0xbe1160e6u));
+    t = fmaf(s, t, __uint_as_float(0x3e4cb8bfu));
+    t = fmaf(s, t, __uint_as_float(0xbeaaaa62u));
+    float r = fmaf(a, s * t, a);                                   // atan(a), a in [0, 1]
+    r = ay > ax ? __uint_as_float(0x3fc90fdbu) - r : r;           // pi / 2 - atan(1 / a)
+    r = __builtin_signbit(x) ? __uint_as_float(0x40490fdbu) - r : r;   // pi - ... (x = -0 included)
+    return copysignf(r, y);
+}
+
 __host__ __device__ constexpr int digit_rev4(int k) {
     return ((k & 3) << 4) | (k & 12) | ((k >> 4) & 3);
 }

@@ -246,30 +246,6 @@ __device__ __forceinline__ float wave_sum_f(float v) {
            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)) +
            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
 }
-// atan2f for the CFO estimates (OFDM.c:798, 821): the device library's atan2f (OCML) without its frexp / ldexp
-// scaling of the quotient and its inf / NaN cases.  For finite normal arguments min(|x|,|y|) * rcp(max) is the
-// library's scaled quotient bit for bit (rcp of a power-of-two-scaled mantissa scales exactly), followed by the
-// same minimax polynomial and quadrant fix-ups, so the result is the library's; (0, 0) gives +-0 as atan2f
-// does for x = +0.
-__device__ __forceinline__ float atan2_cfo(float y, float x) {
-    const float ax = fabsf(x), ay = fabsf(y);
-    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
-    float a = mn * __builtin_amdgcn_rcpf(mx);
-    a = mx > 0.f ? a : 0.f;
-    const float s = a * a;
-    float t = fmaf(s, __uint_as_float(0x3b2d2a58u), __uint_as_float(0xbc7a590cu));
-    t = fmaf(s, t, __uint_as_float(0x3d29fb3fu));
-    t = fmaf(s, t, __uint_as_float(0xbd97d4d7u));
-    t = fmaf(s, t, __uint_as_float(0x3dd931b2u));
-    t = fmaf(s, t, __uint_as_float(0xbe1160e6u));
-    t = fmaf(s, t, __uint_as_float(0x3e4cb8bfu));
-    t = fmaf(s, t, __uint_as_float(0xbeaaaa62u));
-    float r = fmaf(a, s * t, a);                                   // atan(a), a in [0, 1]
-    r = ay > ax ? __uint_as_float(0x3fc90fdbu) - r : r;           // pi / 2 - atan(1 / a)
-    r = x < 0.f ? __uint_as_float(0x40490fdbu) - r : r;           // pi - ...
-    return copysignf(r, y);
-}
-
 // wave-uniform max / min of an int: DPP within each row of 16 lanes (quad xor 1, xor 2, half-row and
 // row mirrors), then the four row results by readlane -- no LDS round trips (a __shfl_xor ladder is six
 // serial ds_bpermute)

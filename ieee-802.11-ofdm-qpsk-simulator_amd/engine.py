@@ -69,6 +69,18 @@ class Engine:
     def synchronize(self):
         check(self.lib, self.lib.ofdm_ctx_synchronize(self.ctx), "synchronize")
 
+    def trim(self) -> int:
+        """Free the context's sweep scratch (ofdm_ctx_trim: up to 6 GiB of frame-sweep hand-off buffer); returns
+        the bytes released.  Later sweeps allocate it again."""
+        n = C.c_int64()
+        check(self.lib, self.lib.ofdm_ctx_trim(self.ctx, C.byref(n)), "ctx_trim")
+        return n.value
+
+    def scratch_bytes(self) -> int:
+        n = C.c_int64()
+        check(self.lib, self.lib.ofdm_ctx_scratch_bytes(self.ctx, C.byref(n)), "ctx_scratch_bytes")
+        return n.value
+
     # ---- timing ----------------------------------------------------------------------
     def timing(self, enable: bool = True):
         check(self.lib, self.lib.ofdm_timing_enable(self.ctx, int(enable)), "timing_enable")

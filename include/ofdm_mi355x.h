@@ -103,6 +103,14 @@ int ofdm_ctx_destroy(ofdm_ctx *ctx);
  * NULL selects the HIP null (default) stream.  A new context uses its own non-blocking stream. */
 int ofdm_ctx_set_stream(ofdm_ctx *ctx, void *hip_stream);
 int ofdm_ctx_synchronize(ofdm_ctx *ctx);
+/* Release the context's sweep scratch (Tx batches of ofdm_symbol_sweep, the frame sweep's sync -> symbol
+ * hand-off buffer of up to 6 GiB, counters, capture staging) after waiting for the context's streams; the
+ * waveform cache and LTF tables stay.  Later calls grow the scratch again on demand.  `released` (optional)
+ * receives the bytes freed.  (The reference holds no device memory; its buffers are stack/heap arrays freed
+ * when Receiver() returns, OFDM.c:941-1165.) */
+int ofdm_ctx_trim(ofdm_ctx *ctx, int64_t *released);
+/* bytes of sweep scratch the context holds now (what ofdm_ctx_trim would release) */
+int ofdm_ctx_scratch_bytes(ofdm_ctx *ctx, int64_t *bytes);
 /* kernel timing: when enabled, every launch of the named kernel is bracketed by HIP events on the
  * launch stream; query returns the summed device time (ms) and launch count since the last reset.
  * kernel ids: 0 = fft64, 1 = tx_symbols, 2 = rx_symbols, 3 = frame_rx */

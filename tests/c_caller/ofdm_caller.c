@@ -33,7 +33,8 @@ typedef void (*entry_fn)(void);
 static const volatile entry_fn k_entry_points[] = {   /* volatile: kept at -O2 */
     (entry_fn)ofdm_abi_version,     (entry_fn)ofdm_last_error,        (entry_fn)ofdm_device_count,
     (entry_fn)ofdm_ctx_create,      (entry_fn)ofdm_ctx_destroy,       (entry_fn)ofdm_ctx_set_stream,
-    (entry_fn)ofdm_ctx_synchronize, (entry_fn)ofdm_timing_enable,     (entry_fn)ofdm_timing_query,
+    (entry_fn)ofdm_ctx_synchronize, (entry_fn)ofdm_ctx_trim,          (entry_fn)ofdm_ctx_scratch_bytes,
+    (entry_fn)ofdm_timing_enable,   (entry_fn)ofdm_timing_query,
     (entry_fn)ofdm_timing_reset,    (entry_fn)ofdm_fft64,             (entry_fn)ofdm_tx_bytes,
     (entry_fn)ofdm_tx_frames,       (entry_fn)ofdm_rx_frames,         (entry_fn)ofdm_set_next_tx,
     (entry_fn)ofdm_txrx_frames,     (entry_fn)ofdm_rx_frames_dump,    (entry_fn)ofdm_symbol_sweep,
@@ -72,6 +73,9 @@ int main(int argc, char **argv) {
     if (!f) { perror(path); return 1; }
     /* the C receiver: capture int(0.307 len), fp32 CFO, C slicer, fp32 taps, Philox capture offset */
     const ofdm_rx_opts opts = {0, 1, 0, 1, -1, 0, {0, 0}};
+    int last_rs = 0;
+    float last_res[3] = {0, 0, 0};
+    int32_t last_ints[4] = {0, 0, 0, 0};
     for (int i = 0; i < 35; ++i) {                          /* SNR_i = 6 + i (OFDM.c:1197) */
         const double snr = 6.0 + i;
         /* Transmission_Over_Air(tx, ota, snr, len) (OFDM.c:635) */
@@ -87,6 +91,9 @@ int main(int argc, char **argv) {
         fprintf(f, "%.1f %d %.9g %.9g %.9g %d %d %d %d", snr, rs, res[0], res[1], res[2], ints[0], ints[1], ints[2],
                 ints[3]);
         for (int b = 0; b < 96 * ints[3]; ++b) fprintf(f, " %d", bits[b]);
+        last_rs = rs;
+        for (int k = 0; k < 3; ++k) last_res[k] = res[k];
+        for (int k = 0; k < 4; ++k) last_ints[k] = ints[k];
         fputc('\n', f);
         snprintf(path, sizeof path, "%s/capture_%d.bin", out, i);
         FILE *c = fopen(path, "wb");
@@ -94,6 +101,27 @@ int main(int argc, char **argv) {
         fclose(c);
     }
     fclose(f);
+    /* the receiver's staging scratch is held by the context until ofdm_ctx_trim releases it */
+    int64_t held = 0, released = -1, after = -1;
+    if ((rc = ofdm_ctx_scratch_bytes(ctx, &held))) return fail("ofdm_ctx_scratch_bytes", rc);
+    if ((rc = ofdm_ctx_trim(ctx, &released))) return fail("ofdm_ctx_trim", rc);
+    if ((rc = ofdm_ctx_scratch_bytes(ctx, &after))) return fail("ofdm_ctx_scratch_bytes", rc);
+    if (held <= 0 || released != held || after != 0) {
+        fprintf(stderr, "ofdm_ctx_trim: held %lld, released %lld, after %lld\n", (long long)held, (long long)released,
+                (long long)after);
+        return 1;
+    }
+    /* the context stays usable: the next Receiver() call grows its scratch again and repeats the last result */
+    {
+        float res[3];
+        int32_t ints[4];
+        if ((rc = ofdm_receiver(ctx, ota + 2 * last_rs, &opts, OFDM_PAYLOAD_MESSAGE, res, ints, NULL, NULL)))
+            return fail("ofdm_receiver after trim", rc);
+        if (ints[0] != last_ints[0] || ints[1] != last_ints[1] || res[0] != last_res[0] || res[2] != last_res[2]) {
+            fprintf(stderr, "receiver after trim differs from the same call before it\n");
+            return 1;
+        }
+    }
     if ((rc = ofdm_ctx_destroy(ctx))) return fail("ofdm_ctx_destroy", rc);
     return nd == 2 ? 0 : 1;
 }

@@ -140,6 +140,56 @@ def test_reference_plotting_script_reads_our_files(pkg, tmp_path):
     assert (base / "results" / "ber_vs_snr.png").exists()
 
 
+REF_SCRIPTS = ROOT.parent / "reference" / "scripts"
+GPU_KAT_FILE = GOLDEN / "gpu_kat_Code_Output.txt"
+
+
+def _run_compare_double(cwd, code_output_text):
+    """scripts/compare_double.py unchanged, as its __main__ runs it: Code_Output.txt against
+    Matlab_Output.txt in the current directory with tolerance 1e-6 (compare_double.py:41-42)."""
+    import shutil
+    cwd.mkdir(parents=True, exist_ok=True)
+    shutil.copy(REF_SCRIPTS / "compare_double.py", cwd)
+    shutil.copy(ROOT.parent / "reference" / "data" / "Matlab_Output.txt", cwd)
+    (cwd / "Code_Output.txt").write_text(code_output_text)
+    r = subprocess.run([sys.executable, "compare_double.py"], cwd=cwd, capture_output=True, text=True,
+                       env={"PATH": "/usr/bin:/bin"})
+    assert r.returncode == 0, r.stderr
+    return r.stdout
+
+
+def _assert_compare_double_clean(out):
+    assert out.count("Extracted 96 numbers.") == 2, out          # equal lengths: no early return
+    assert "Files have different lengths" not in out
+    assert "Max Error: 0.000000e+00" in out, out
+    assert "Average Error: 0.000000e+00" in out, out
+    assert "Mismatch" not in out, out
+
+
+@pytest.mark.skipif(not (REF_SCRIPTS / "compare_double.py").exists(),
+                    reason="reference scripts only exist in the build container")
+def test_reference_compare_double_reads_our_code_output(pkg, oracle, tmp_path):
+    """north_star: scripts/compare_*.py drop in unchanged.  The KAT receiver's bits (frame mode, MATLAB
+    convention, Tester payload, noiseless capture [0, 3000): D6) written by fileio.write_bits_file are
+    diffed by the unmodified compare_double.py against data/Matlab_Output.txt: zero mismatches.
+    (a) bits of the oracle's KAT receiver (equal to the GPU's: tests/test_gpu_frame.py::test_matlab_known_answer);
+    (b) the Code_Output.txt the GPU KAT test wrote on an MI355X (tests/golden/gpu_kat_Code_Output.txt)."""
+    from ofdm_amd import fileio
+    tb = oracle.tester_bits()
+    w = oracle.frame_waveform(tb, "matlab", False, 10)
+    o = oracle.receiver_frame(w[:3000], tb, "matlab")
+    p = tmp_path / "bits.txt"
+    fileio.write_bits_file(o["bits"][:96], p)
+    _assert_compare_double_clean(_run_compare_double(tmp_path / "a", p.read_text()))
+    assert GPU_KAT_FILE.exists(), "the GPU KAT record is committed with the tests"
+    _assert_compare_double_clean(_run_compare_double(tmp_path / "b", GPU_KAT_FILE.read_text()))
+    # the check is not vacuous: one flipped bit is reported as a mismatch
+    bad = p.read_text().split("\t")
+    bad[5] = str(1 - int(bad[5]))
+    out = _run_compare_double(tmp_path / "c", "\t".join(bad))
+    assert "Mismatch at index 5" in out and "Max Error: 1.000000e+00" in out
+
+
 def test_shard_ranges(pkg):
     from ofdm_amd import dist
     for n in (0, 1, 7, 1000, 10 ** 7 + 3):
