@@ -224,6 +224,16 @@ static __device__ unsigned long long g_pack_stamps[4][8];
 #ifndef PACK_SACC_SUB
 #define PACK_SACC_SUB 1     // the same for the ideal-CSI receiver (2 copies spill it at its 168-VGPR budget)
 #endif
+// A/B options: the SNR iteration's five counter terms wave-reduced by DPP and added by one lane (flush_wave,
+// ofdm_rxcommon.h) instead of 64 same-address LDS atomics per term (flush_lanes).  Negative (round 5,
+// profiles/r05/ab/wave_flush.txt): c2 -5.2 %, c3 -7.0 %, c5 -1.1 % -- the serialised atomics run in the LDS pipe
+// beside the VALU stream, the ~70 VALU of the reduction do not
+#ifndef OFDM_PACK_WAVE_FLUSH_IDEAL
+#define OFDM_PACK_WAVE_FLUSH_IDEAL 0
+#endif
+#ifndef OFDM_PACK_WAVE_FLUSH_LS
+#define OFDM_PACK_WAVE_FLUSH_LS 0
+#endif
 template <int KIND, int CONV, int CHAN, bool DUMP>
 __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFDM_RX_PACK_FADE_WAVES : OFDM_RX_PACK_WAVES)
                                             : OFDM_RX_PACK_IDEAL_WAVES) void rx_pack_kernel(RxArgs a) {
@@ -251,7 +261,9 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
     // flush_lanes' five slots per SNR point; for the first SACC_XQ points SUBN - 1 more copies: lane l adds into
     // copy l % SUBN, so that an SNR iteration's 5 x 64 same-address LDS atomics (the kernel's LDS bank-conflict
     // cycles) spread over SUBN addresses in distinct banks; the copies are summed before the flush
-    constexpr int SUBN = KIND != 2 ? PACK_SACC_SUB : FADE ? (PACK_SACC_SUB_LS < 4 ? PACK_SACC_SUB_LS : 4) : PACK_SACC_SUB_LS;
+    constexpr bool WFLUSH = KIND == 2 ? OFDM_PACK_WAVE_FLUSH_LS : OFDM_PACK_WAVE_FLUSH_IDEAL;
+    constexpr int SUBN = WFLUSH ? 1 : KIND != 2 ? PACK_SACC_SUB : FADE ? (PACK_SACC_SUB_LS < 4 ? PACK_SACC_SUB_LS : 4)
+                                                                  : PACK_SACC_SUB_LS;
     constexpr int SACC_XQ = 16;
     __shared__ unsigned long long sacc[OFDM_MAX_SNR][5];
     __shared__ unsigned long long sacx[SUBN > 1 ? SACC_XQ : 1][SUBN > 1 ? 5 * (SUBN - 1) : 1];
@@ -776,9 +788,13 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
                     dbit1[0] = db1[0]; dbit1[1] = db1[1]; dbit1[2] = db1[2];
                 }
             }
-            FrameAcc acc;
-            frame_metrics(acc, KIND == 2 ? 4.0f * evm : evm, be, ax);
-            flush_lanes(acc, valid, slots(q, SPLIT ? lane_fresh() : lane));
+            if constexpr (WFLUSH) {
+                flush_wave(KIND == 2 ? 4.0f * evm : evm, be, ax, valid, lane, sacc[q]);
+            } else {
+                FrameAcc acc;
+                frame_metrics(acc, KIND == 2 ? 4.0f * evm : evm, be, ax);
+                flush_lanes(acc, valid, slots(q, SPLIT ? lane_fresh() : lane));
+            }
             }   // !SPLIT
         }
         PK_STAMP(4);                                     // SNR loop
