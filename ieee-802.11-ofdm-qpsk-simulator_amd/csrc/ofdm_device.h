@@ -182,11 +182,25 @@ __device__ __forceinline__ void philox10_c2_vk(const PhiloxHead &h, const uint32
     for (int b = 0; b < NB; ++b) out[b] = make_uint4(c0[b], c1[b], c2[b], c3[b]);
 }
 
+// The Box-Muller angle of a Philox word x, in revolutions (v_sin / v_cos take revolutions).
+// OFDM_BM_ANGLE_BITS (A/B option): 1 + (x >> 9) 2^-23 in [1, 2) built by one v_alignbit (the exponent bits
+// shifted in from a constant) instead of v_cvt_f32_u32 + v_mul.
+#ifndef OFDM_BM_ANGLE_BITS
+#define OFDM_BM_ANGLE_BITS 0
+#endif
+__device__ __forceinline__ float bm_angle(uint32_t x) {
+#if OFDM_BM_ANGLE_BITS
+    return __uint_as_float(__builtin_amdgcn_alignbit(0x7Fu, x, 9));
+#else
+    return (float)x * 0x1p-32f;
+#endif
+}
+
 // Box-Muller pair.  u1 = fma((float)x1, 2^-32, 2^-33) in (0, 1] (tail to 6.7 sigma);
 // u2 = (float)x2 * 2^-32 in revolutions.  Same quantisation as oracle/ofdm_oracle.c:bm_pair.
 __device__ __forceinline__ float2 box_muller(uint32_t x1, uint32_t x2) {
     const float u1 = fmaf((float)x1, 0x1p-32f, 0x1p-33f);
-    const float u2 = (float)x2 * 0x1p-32f;
+    const float u2 = bm_angle(x2);
     // -2 ln(u1) = -2 ln(2) log2(u1)
     const float r = __builtin_amdgcn_sqrtf(-1.38629436111989061883f * __builtin_amdgcn_logf(u1));
     return make_float2(r * __builtin_amdgcn_cosf(u2), r * __builtin_amdgcn_sinf(u2));
@@ -212,8 +226,8 @@ __device__ __forceinline__ Gauss4 gauss4(uint32_t c0, uint32_t c1, uint32_t c2, 
 }
 
 __device__ __forceinline__ Noise4 noise4_of(uint4 o, float K) {
-    const float u1a = fmaf((float)o.x, 0x1p-32f, 0x1p-33f), u2a = (float)o.y * 0x1p-32f;
-    const float u1b = fmaf((float)o.z, 0x1p-32f, 0x1p-33f), u2b = (float)o.w * 0x1p-32f;
+    const float u1a = fmaf((float)o.x, 0x1p-32f, 0x1p-33f), u2a = bm_angle(o.y);
+    const float u1b = fmaf((float)o.z, 0x1p-32f, 0x1p-33f), u2b = bm_angle(o.w);
     Noise4 n;
     n.r0 = __builtin_amdgcn_sqrtf(K * __builtin_amdgcn_logf(u1a));
     n.r1 = __builtin_amdgcn_sqrtf(K * __builtin_amdgcn_logf(u1b));

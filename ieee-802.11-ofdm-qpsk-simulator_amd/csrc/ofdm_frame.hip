@@ -481,6 +481,28 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// LDS conflict attribution probes (diagnostic builds only, tools/lds_attrib.py; results unchanged): FRAME_DUP_<SITE>
+// issues one access site's LDS instructions a second time, same instruction form and lane addresses, waited for at
+// once, so that the PMC deltas of SQ_INSTS_LDS / SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE against the plain build
+// are that site's instructions and their conflict and array cycles
+__device__ __forceinline__ void dup_read2_b32(const float *p) {
+    typedef float f2d __attribute__((ext_vector_type(2)));
+    f2d d;
+    asm volatile("ds_read2_b32 %0, %1 offset1:1\n\ts_waitcnt lgkmcnt(0)" : "=v"(d)
+                 : "v"((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float *)p));
+}
+__device__ __forceinline__ void dup_read_b32(const float *p) {
+    float d;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(d)
+                 : "v"((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float *)p));
+}
+__device__ __forceinline__ void dup_write_b128(float *p, float4 v) {
+    typedef float f4d __attribute__((ext_vector_type(4)));
+    f4d d = {v.x, v.y, v.z, v.w};
+    asm volatile("ds_write_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" :: "v"((uint32_t)(uintptr_t)(__attribute__((address_space(3))) float *)p),
+                 "v"(d) : "memory");
+}
+
 // x mod the table period for 0 <= x < 2^14 (q = floor(x / period) by multiply-high: exact there)
 struct ImMod {
     int period;
@@ -493,16 +515,46 @@ struct ImMod {
 
 // N (odd) contiguous LDS floats x[k] = p[s + k] as (N - 1) / 2 ds_read_b64 + 1 ds_read_b32; ODD = s & 1 (uniform
 // per item), so the pairs are 8-byte aligned
-template <int ODD, int N>
+// The pairs are read through an 8-byte vector type in the LDS address space, so that each is one ds_read_b64
+// (64 banks of 4 B, 2 LDS cycles per wave-instruction) and not a ds_read2_b32 (two 32-bank dword accesses, 4
+// cycles): the matched filter's lane starts are 10 floats apart, which puts lanes u and u + 16 on one bank of a
+// 32-bank dword access (2-way) and the runs of different needed ranges on further shared banks -- 7.7 conflict
+// cycles per ds_read2_b32 in the sync kernel (profiles/r05/lds_attrib.json, tools/ubench_lds_item.hip).
+// FORM 0: float2 loads (the compiler pairs them into ds_read2_b32), 1: 8-byte vector loads (paired into
+// ds_read2_b64: two 16-lane accesses per half, 32 banks), 2: the same with a base VGPR per load so that they stay
+// single ds_read_b64 (A/B on the reference sweep, profiles/r05/ab/mf_load_forms.txt: 0 -> 1 +0.4 %, -> 2 +0.6 %,
+// conflict cycles 479 -> 351 per item).  The fixed-geometry kernel uses 2; the generic ones 1 (2 spills them at
+// their 168-VGPR budget).
+#ifndef FRAME_MF_B64
+#define FRAME_MF_B64 2
+#endif
+#ifndef FRAME_MF_B64_GEN
+#define FRAME_MF_B64_GEN 1
+#endif
+template <int ODD, int FORM, int N>
 __device__ __forceinline__ void lds_readn(const float *p, int s, float (&x)[N]) {
     static_assert(N & 1, "odd window");
     if constexpr (ODD) x[0] = p[s];
-    const float2 *q = reinterpret_cast<const float2 *>(p + s + ODD);
+    typedef const __attribute__((address_space(3))) f2v lf2c;
+    lf2c *q = (lf2c *)(p + s + ODD);                     // 8-byte aligned: the caller picks ODD = parity of s
+    const float2 *qf = reinterpret_cast<const float2 *>(p + s + ODD);
 #pragma unroll
     for (int m = 0; m < (N - 1) / 2; ++m) {
-        const float2 w = q[m];                           // floats s + ODD + 2m, s + ODD + 2m + 1
-        x[ODD + 2 * m] = w.x;
-        x[ODD + 2 * m + 1] = w.y;
+        float wx, wy;                                    // floats s + ODD + 2m, s + ODD + 2m + 1
+        if constexpr (FORM == 2) {
+            lf2c *qm = q + m;
+            opaque(qm);
+            const f2v w = *qm;
+            wx = w.x; wy = w.y;
+        } else if constexpr (FORM == 1) {
+            const f2v w = q[m];
+            wx = w.x; wy = w.y;
+        } else {
+            const float2 w = qf[m];
+            wx = w.x; wy = w.y;
+        }
+        x[ODD + 2 * m] = wx;
+        x[ODD + 2 * m + 1] = wy;
     }
     if constexpr (!ODD) x[N - 1] = p[s + N - 1];
 }
@@ -562,7 +614,12 @@ __device__ __forceinline__ void capture_blocks(const A &a, int wave_len, float *
         // samples of the block outside [0, L) land in the region's slack, never read as capture
 #pragma unroll
         for (int u = 0; u < FRAME_CAP_U; ++u)
-            if (bb + 64 * u <= be) *reinterpret_cast<float4 *>(rbase + 4 * (bb + 64 * u - b0)) = v[u];
+            if (bb + 64 * u <= be) {
+                *reinterpret_cast<float4 *>(rbase + 4 * (bb + 64 * u - b0)) = v[u];
+#ifdef FRAME_DUP_CAP
+                dup_write_b128(rbase + 4 * (bb + 64 * u - b0), v[u]);
+#endif
+            }
     }
 }
 
@@ -577,6 +634,7 @@ __device__ __forceinline__ void capture_blocks(const A &a, int wave_len, float *
 template <int FIX_ND, int FIX_CAP, int W = SYNC_WAVES>
 __global__ __launch_bounds__(64 * W, FRAME_SYNC_MINW) void frame_sync_kernel(FrameArgs a) {
     constexpr bool FIX = FIX_ND > 0;
+    constexpr int MF_FORM = FIX ? FRAME_MF_B64 : FRAME_MF_B64_GEN;   // matched-filter load form (lds_readn)
     constexpr int SYNC_WAVES = W, SYNC_THREADS = 64 * W;      // this instantiation's block
     static_assert(FIX == (FIX_CAP > 0), "both or neither");
     extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
@@ -756,6 +814,13 @@ __global__ __launch_bounds__(64 * W, FRAME_SYNC_MINW) void frame_sync_kernel(Fra
                     constexpr int j = decltype(jc)::value;
 #pragma unroll
                     for (int k = 0; k < DET_B; ++k) { xr[j][k] = tr_[DET_B * j + k]; xi[j][k] = ti_[DET_B * j + k]; }
+#ifdef FRAME_DUP_DET
+#pragma unroll
+                    for (int k = 0; k < DET_B; k += 2) {
+                        dup_read2_b32((const float *)(tr_ + DET_B * j + k));
+                        dup_read2_b32((const float *)(ti_ + DET_B * j + k));
+                    }
+#endif
                 };
                 load_blk(std::integral_constant<int, 0>{});
                 load_blk(std::integral_constant<int, 1>{});
@@ -820,6 +885,12 @@ __global__ __launch_bounds__(64 * W, FRAME_SYNC_MINW) void frame_sync_kernel(Fra
             static_for<0, 2>([&](auto r2c) {
                 constexpr int r2 = decltype(r2c)::value;
                 if (r2 < R) {
+#ifdef FRAME_DUP_BP
+                    {
+                        int d;
+                        asm volatile("ds_bpermute_b32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(d) : "v"(owner * 4), "v"((int)(uint32_t)cm[r2]));
+                    }
+#endif
                     const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)cm[r2], owner, 64);
                     const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(cm[r2] >> 32), owner, 64);
                     if (rp == r2) w = ((unsigned long long)hi << 32) | lo;
@@ -935,8 +1006,8 @@ __global__ __launch_bounds__(64 * W, FRAME_SYNC_MINW) void frame_sync_kernel(Fra
             if (n >= 20 && n < L) {                              // all 21 taps inside the capture
                 float xr[21], xi[21];                            // x[20 - t] = sample n - t
                 const int si = im_mod(im0 + n - 20);
-                if (par_r) lds_readn<1>(rbase, off + n - 20, xr); else lds_readn<0>(rbase, off + n - 20, xr);
-                if (par_i) lds_readn<1>(imt, si, xi); else lds_readn<0>(imt, si, xi);
+                if (par_r) lds_readn<1, MF_FORM>(rbase, off + n - 20, xr); else lds_readn<0, MF_FORM>(rbase, off + n - 20, xr);
+                if (par_i) lds_readn<1, MF_FORM>(imt, si, xi); else lds_readn<0, MF_FORM>(imt, si, xi);
                 v = make_float2(xr[10] * tv[10], xi[10] * tv[10]);
 #pragma unroll
                 for (int tt = 0; tt < 10; ++tt) {
@@ -985,8 +1056,17 @@ __global__ __launch_bounds__(64 * W, FRAME_SYNC_MINW) void frame_sync_kernel(Fra
                 if (n_lo >= 0 && p + 2 * (e - 1) < L) {
                     float xr[MF_W], xi[MF_W];                    // x[k] = sample n_lo + k
                     const int si = im_mod(im0 + n_lo);
-                    if (par_r) lds_readn<1>(rbase, off + n_lo, xr); else lds_readn<0>(rbase, off + n_lo, xr);
-                    if (par_i) lds_readn<1>(imt, si, xi); else lds_readn<0>(imt, si, xi);
+                    if (par_r) lds_readn<1, MF_FORM>(rbase, off + n_lo, xr); else lds_readn<0, MF_FORM>(rbase, off + n_lo, xr);
+                    if (par_i) lds_readn<1, MF_FORM>(imt, si, xi); else lds_readn<0, MF_FORM>(imt, si, xi);
+#ifdef FRAME_DUP_MF
+#pragma unroll
+                    for (int m = 0; m < (MF_W - 1) / 2; ++m) {
+                        dup_read2_b32(rbase + off + n_lo + par_r + 2 * m);
+                        dup_read2_b32(imt + si + par_i + 2 * m);
+                    }
+                    dup_read_b32(rbase + off + n_lo + (par_r ? 0 : MF_W - 1));
+                    dup_read_b32(imt + si + (par_i ? 0 : MF_W - 1));
+#endif
 #pragma unroll
                     for (int o = 0; o < MF_RUN; ++o) {           // output at sample n_lo + 2 o + 20
                         if (s0 + o < e) {
@@ -1015,6 +1095,12 @@ __global__ __launch_bounds__(64 * W, FRAME_SYNC_MINW) void frame_sync_kernel(Fra
         // every fr[] sample the estimates read, loaded in one LDS round trip (lanes >= 16 read the coarse window
         // too, and drop it)
         const float2 cu = fr[80 + (lx & 15)], cw = fr[96 + (lx & 15)], l1 = fr[192 + lx], l2 = fr[256 + lx];
+#ifdef FRAME_DUP_CFO
+        dup_read2_b32((const float *)&fr[80 + (lx & 15)]);
+        dup_read2_b32((const float *)&fr[96 + (lx & 15)]);
+        dup_read2_b32((const float *)&fr[192 + lx]);
+        dup_read2_b32((const float *)&fr[256 + lx]);
+#endif
         float2 d0 = make_float2(0.f, 0.f), d1 = d0;          // the reference frame's data windows, for the hand-off
         if constexpr (FIX && FIX_ND == 2) {
             d0 = fr[336 + lx];

@@ -167,7 +167,10 @@ __device__ __forceinline__ void demap_bin(float2 u, float r, uint32_t &t, uint32
 // Ablation builds (diagnostics only, results are wrong; their run time against the real kernel prices a
 // stage including its stalls): OFDM_ABL_NO_PHILOX replaces the Philox rounds by one multiply,
 // OFDM_ABL_NO_BM the Box-Muller transcendentals by multiplies, OFDM_ABL_NO_PREPASS transforms the clean
-// symbols of a block's first group only.
+// symbols of a block's first group only.  For the per-stage instruction budget of the SNR loop (tools/stage_mix.py,
+// static counts of the assembly): OFDM_ABL_NO_DFFT drops the data windows' 64-point FFT (the noise samples go to
+// the bin pairs untransformed), OFDM_ABL_NO_LFFT the LTF pair's 32-point FFT, OFDM_ABL_NO_EQ replaces each bin
+// pair's estimate / equaliser / slicer / demap by one sum, OFDM_ABL_NO_CNT drops frame_metrics + the LDS flush.
 template <typename KS>
 __device__ __forceinline__ Noise4 pack_noise(const PhiloxHead &hd, uint32_t c2, const KS &keys, uint32_t k1, float K) {
 #ifdef OFDM_ABL_NO_PHILOX
@@ -502,16 +505,20 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
                         z[m + 16] = make_float2(hi.r0 * hi.c0, -(hi.r0 * hi.s0));
                         z[m + 17] = make_float2(hi.r1 * hi.c1, -(hi.r1 * hi.s1));
                     });
+#ifndef OFDM_ABL_NO_LFFT
                     static_for<0, 4>([&](auto jc) {
                         constexpr int j = 4 * i + decltype(jc)::value;
                         const float2 u = z[j], v = z[j + 16];
                         z[j] = cadd(u, v);
                         z[j + 16] = twiddle<2 * j, false>(csub(u, v));     // W32^j
                     });
+#endif
                     sched_fence();
                 });
+#ifndef OFDM_ABL_NO_LFFT
                 dif4<false, 16, 0>(z);
                 dif4<false, 16, 16>(z);
+#endif
                 // E'[k] = (Z[k] + conj Z[-k]) / 2 - j W64^k (Z[k] - conj Z[-k]) / 2 (Z indices mod 32), kept
                 // as 2 E'[k] per pair (48 VGPRs instead of the 62 of Z); E'[64 - k] = conj E'[k]
                 static_for<0, PACK_PAIRS>([&](auto pc) {
@@ -667,7 +674,9 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
 #endif
                     if constexpr (Q % OFDM_PACK_GEN_SPLIT == OFDM_PACK_GEN_SPLIT - 1 && Q < 3) sched_fence();
                 });
+#ifndef OFDM_ABL_NO_DFFT
                 static_for<0, 4>([&](auto ic) { dif_stage1<false, 4 * g + decltype(ic)::value>(x); });
+#endif
                 sched_fence();
             });
             // ---- bin pairs: noise split, clean spectra, estimate, equaliser, demap of both data symbols
@@ -733,6 +742,14 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
                 const float2 y1m = make_float2(fmaf(0.5f, B.y, c1.z), fmaf(0.5f, B.x, c1.w));
                 float2 u0k, u0m, u1k, u1m;
                 float rk = 0.f, rm = 0.f;
+#ifdef OFDM_ABL_NO_EQ
+                if constexpr (true) {
+                    const float4 e4 = pe4[slot];
+                    evm += (y0k.x + y0m.y) + (y1k.x + y1m.y) + e4.x;
+                    if constexpr (p < EE_LDS_FIRST) evm += ee[p].x;
+                    (void)t0; (void)t1; (void)sm; (void)u0k; (void)u0m; (void)u1k; (void)u1m; (void)rk; (void)rm;
+                } else
+#endif
                 if constexpr (KIND == 2) {
                     float ex, ey;
                     if constexpr (p < EE_LDS_FIRST) {
@@ -755,10 +772,12 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
                     constexpr float cs = (CONV == OFDM_CONV_C && (k & 1)) ? -1.0f : 1.0f;   // k, k2 same parity
                     u0k = cscale(y0k, cs); u0m = cscale(y0m, cs); u1k = cscale(y1k, cs); u1m = cscale(y1m, cs);
                 }
+#ifndef OFDM_ABL_NO_EQ
                 demap_bin<KIND, DUMP>(u0k, rk, t0, sm, evm, em, data_index(k), deq0, db0);
                 demap_bin<KIND, DUMP>(u0m, rm, t0, sm, evm, em, data_index(k2), deq0, db0);
                 demap_bin<KIND, DUMP>(u1k, rk, t1, sm, evm, em, data_index(k), deq1, db1);
                 demap_bin<KIND, DUMP>(u1m, rm, t1, sm, evm, em, data_index(k2), deq1, db1);
+#endif
                 if constexpr ((p & 3) == 3) {
                     // 16 decisions: im errors at even bit positions, re errors at odd
                     ax += __popc(em);
@@ -773,21 +792,32 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
 #endif
                 if constexpr (p % OFDM_PACK_FENCE_PAIRS == OFDM_PACK_FENCE_PAIRS - 1) sched_fence();
             };
-            dif_sub16<false, 0>(x);
+#ifdef OFDM_ABL_NO_DFFT
+#define PK_SUB16(R) do { } while (0)
+#else
+#define PK_SUB16(R) dif_sub16<false, R>(x)
+#endif
+            PK_SUB16(0);
             static_for<0, 6>(pair);
             sched_fence();
-            dif_sub16<false, 2>(x);
+            PK_SUB16(2);
             static_for<6, 13>(pair);
             sched_fence();
-            dif_sub16<false, 1>(x);
-            dif_sub16<false, 3>(x);
+            PK_SUB16(1);
+            PK_SUB16(3);
             static_for<13, 24>(pair);
+#undef PK_SUB16
             if constexpr (DUMP) {
                 if (dbit0) {
                     dbit0[0] = db0[0]; dbit0[1] = db0[1]; dbit0[2] = db0[2];
                     dbit1[0] = db1[0]; dbit1[1] = db1[1]; dbit1[2] = db1[2];
                 }
             }
+#ifdef OFDM_ABL_NO_CNT
+            if constexpr (true) {
+                asm volatile("" :: "v"(evm), "v"(be), "v"(ax), "v"(valid ? 1 : 0));
+            } else
+#endif
             if constexpr (WFLUSH) {
                 flush_wave(KIND == 2 ? 4.0f * evm : evm, be, ax, valid, lane, sacc[q]);
             } else {
