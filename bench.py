@@ -17,6 +17,9 @@ Workloads (BASELINE.json configs; --workload):
                            AWGN (every config uses the reference's real-only noise)
   frame                    the reference's own trial (sync, CFO, LS): the like-for-like line next
                            to the reference's trial loop on the host
+  fft64                    K1 alone (ofdm_fft64, OFDM.c fft()/ifft() :282-339): 2^24 64-point transforms per launch,
+                           a step = one fft + one ifft over the HBM-resident batch; HBM roofline at 1,024 B per
+                           transform (512 B read + 512 B written); units are transforms (one OFDM symbol each)
 
 Launched as `python bench.py --gpus N --steps K --warmup W`, or for N > 1 under
 `torch.distributed.run` (one rank per GPU, RCCL all-reduce).  Rank 0 prints ONE JSON line.
@@ -70,7 +73,10 @@ WORKLOADS = {
     "frame8": ("frame mode with a 96-character message (8 data symbols per frame, 5955-sample captures: the long-"
                "message path); units are data symbols x SNR points",
                dict(payload="message", noise="real", conv="c"), 1_000_000, "weak"),
+    "fft64": ("K1: batched 64-point fft() + ifft() (C convention) of HBM-resident symbols, 2^24 transforms per "
+              "launch", {}, 1 << 24, "weak"),
 }
+FFT_BYTES_PER_TRANSFORM = 1024     # 64 complex f32 read + 64 written
 # data symbols per frame (trial) of each workload; frame8 sets its message before the sweep
 FRAME_DATA = {"frame8": 8}
 FRAME8_MESSAGE = (b"The quick brown fox jumps over the lazy dog; 802.11a OFDM-QPSK frames on MI355X, eight symbols.. ")[:96]
@@ -256,6 +262,8 @@ def cpu_baseline(workload: str, seconds: float = 12.0, share: dict | None = None
     except Exception as e:  # pragma: no cover
         return {"value": None, "unit": "OFDM symbols/s", "cores": 0, "kind": "reference",
                 "sample": f"unavailable: {e}"}
+    if workload == "fft64":
+        return cpu_baseline_fft(ref, seconds, share)
     frame = workload.startswith("frame")     # frame8: the reference has only its own 2-symbol message
     rayleigh = workload == "c5"
     ideal = workload == "c2"
@@ -293,6 +301,37 @@ def cpu_baseline(workload: str, seconds: float = 12.0, share: dict | None = None
             "cores_source": f"{P} = min(sched_getaffinity {share['affinity']}, {share['source']})",
             "cores_note": ("measured on the job's whole host share; CPUs outside it belong to other jobs "
                            "and are not used (no extrapolation)"),
+            "single_core": single}
+
+
+def _fft_worker(args):
+    """The reference's fft() then ifft() on n vectors: (transforms, seconds, checksum)."""
+    n, seed = args
+    from oracle import RefLib  # noqa: PLC0415  (bench.py's cpu_baseline leg only)
+    r = RefLib()
+    t1, c1 = r.time_fft(n, False, seed=seed)
+    t2, c2 = r.time_fft(n, True, seed=seed)
+    return 2 * n, t1 + t2, c1 + c2
+
+
+def cpu_baseline_fft(ref, seconds: float, share: dict | None) -> dict:
+    """fft64: the reference's own fft() / ifft() (OFDM.c:282-339, gcc -O2) on the host, one process per CPU of the
+    job's share and on one thread, the same alternation of fft and ifft as the GPU step."""
+    t, _ = ref.time_fft(20000, False)
+    per = max(t / 20000, 1e-9)
+    share = share or host_cpu_share()
+    P = share["cores"]
+    n1 = max(1000, int(seconds / 6 / per))
+    u1, t1, _ = _fft_worker((n1, 7))
+    single = {"value": u1 / t1, "unit": "OFDM symbols/s", "cores": 1, "kind": "reference",
+              "sample": f"{n1} fft() + {n1} ifft() calls of src/OFDM.c on 64 samples, 1 thread, {t1:.1f} s"}
+    n = max(1000, int(seconds / 3 / per))
+    units, wall, _ = _parallel(_fft_worker, [(n, 1000 + k) for k in range(P)])
+    return {"value": units / wall, "unit": "OFDM symbols/s", "cores": P, "kind": "reference",
+            "sample": f"{P} x ({n} fft() + {n} ifft()) of src/OFDM.c on 64 samples in {wall:.1f} s wall on {P} host "
+                      "processes started together (start-up untimed)",
+            "cpu_model": cpu_model(), "cpus_visible": share["visible"],
+            "cores_source": f"{P} = min(sched_getaffinity {share['affinity']}, {share['source']})",
             "single_core": single}
 
 
@@ -358,6 +397,90 @@ class PipelinedSymbolStep:
             rx_done[k].record(s_rx)
 
 
+def run_fft64(args, cpu, torch, dist, pkg, abi, codeobj, rank, world, dev, distributed):
+    """--workload fft64: K1 (ofdm_fft64) alone on an HBM-resident batch of 2^24 symbols per GPU (weak scaling).  A
+    step is fft() of the batch into a second buffer and ifft() back (C convention, OFDM.c:314-339): two launches,
+    2^25 transforms.  The roofline is HBM: 1,024 algorithmic bytes per transform over the launches' HIP-event time
+    against 8 TB/s; `traffic` is the PMC-measured FETCH_SIZE x 2 + WRITE_SIZE per launch when a record of this build
+    exists (profiles/pmc_summary.json["fft64"])."""
+    desc, _, n, scaling = WORKLOADS["fft64"]
+    if args.symbols:
+        n = args.symbols
+    eng = pkg.Engine(dev)
+    g = torch.Generator(device=f"cuda:{dev}").manual_seed(0x80211A + rank)
+    x = torch.randn((n, 64), dtype=torch.complex64, device=f"cuda:{dev}", generator=g)
+    y = torch.empty_like(x)
+    done = torch.zeros(1, dtype=torch.int64, device=f"cuda:{dev}")
+
+    def step():
+        eng.fft64_into(x, y, inverse=False)
+        eng.fft64_into(y, x, inverse=True)
+        if distributed:
+            dist.all_reduce(done, op=dist.ReduceOp.SUM)      # the job's one collective (a completion count)
+
+    x0 = x[:4].clone()
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    eng.timing(True)
+    eng.timing_reset()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    eng.timing(False)
+    ms, launches = eng.timing_query(abi.K_FFT)
+    if distributed:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    # ifft(fft(x)) in the reference's C convention is x circularly shifted by 32 samples (fftshift of the IDFT,
+    # SURVEY D5): after an odd number of steps the first vectors are x0 rolled by 32, after an even number x0 (a
+    # cheap check that the launches did the work)
+    want = x0.roll(32, dims=1) if (args.warmup + args.steps) % 2 else x0
+    rt_err = float((x[:4] - want).abs().max() / x0.abs().max())
+    units_per_launch = float(n)
+    avg_s = ms / max(launches, 1) / 1e3
+    achieved = units_per_launch * FFT_BYTES_PER_TRANSFORM / avg_s / 1e9
+    pmc = load_pmc("fft64")
+    lib_id = codeobj.workload_build_id(abi.library_file(), "fft64")
+    cert, why = certify_pmc(pmc, "fft64_lds_kernel", lib_id)
+    tpu = cert.get("hbm_bytes_per_unit")
+    value = 2.0 * n * world * args.steps / elapsed
+    if rank == 0:
+        line = {
+            "metric": "OFDM symbols/sec (whole node) over BER-vs-SNR sweep; achieved HBM GB/s vs peak",
+            "value": value, "unit": "OFDM symbols/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True, "scaling": scaling,
+            "vs_baseline": None, "dtype": "f32", "data": "synthetic (torch.randn complex64, seed 0x80211A + rank)",
+            "config": {"workload": "fft64", "description": desc, "transforms_per_launch_per_gpu": n,
+                       "launches_per_step": 2, "conv": "c",
+                       "parallelism": (f"dp{world} (each rank its own batch, weak scaling)" if distributed
+                                       else "1 process, no collective (not launched under torchrun)")},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": tpu * units_per_launch if tpu else None,
+                         "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x 2 + WRITE_SIZE)",
+                         **({"traffic_null_reason": why} if not tpu else {}),
+                         "algorithmic_bytes_per_unit": FFT_BYTES_PER_TRANSFORM, "kernel": "fft64_lds_kernel",
+                         "avg_launch_ms": avg_s * 1e3, "launches": launches, "units_per_launch": units_per_launch,
+                         "lib_build_id": lib_id, "pmc_build_id": pmc.get("build_id")},
+            "results": {"fft_ifft_roundtrip_max_rel_err": rt_err},
+        }
+        if cpu is not None:
+            line["cpu_baseline"] = cpu
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if distributed:
+        dist.destroy_process_group()
+
+
 def wants_cpu_baseline(args) -> bool:
     """Rank 0 of the job times the reference (any WORLD_SIZE); the others do not."""
     return int(os.environ.get("RANK", "0")) == 0 and not args.no_cpu_baseline
@@ -396,6 +519,9 @@ def main():
         odist.init_from_env("nccl")
     dev = local if distributed else 0
 
+    if args.workload == "fft64":
+        run_fft64(args, cpu, torch, dist, pkg, abi, codeobj, rank, world, dev, distributed)
+        return
     desc, kw, symbols, scaling = WORKLOADS[args.workload]
     if args.symbols:
         symbols = args.symbols

@@ -318,6 +318,7 @@ __device__ __forceinline__ void sched_fence() {}
 // global-address-space views (keep loads global_* after opaque(), which erases provenance).
 // Native clang vectors, not float2 (HIP_vector_type's members are not address-space qualified).
 typedef float f2v __attribute__((ext_vector_type(2)));
+typedef float f4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const f2v gcf2;
 typedef __attribute__((address_space(1))) f2v gf2;
 __device__ __forceinline__ float2 gld(gcf2 *p, int i) { const f2v v = p[i]; return make_float2(v.x, v.y); }

@@ -199,9 +199,16 @@ __device__ __forceinline__ float2 dpp_f2(float2 v) {
     return make_float2(__int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v.x), CTRL, 0xF, 0xF, false)),
                        __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v.y), CTRL, 0xF, 0xF, false)));
 }
+#ifndef OFDM_K1_NT
+#define OFDM_K1_NT 1        // non-temporal HBM stores (K1; A/B round 5, profiles/r05/ab/k1.txt: LDS kernel +1.7 % with
+                            // <= 128 VGPRs; the quad kernel's scattered 8-byte stores fall to 2.0e9 with them)
+#endif
+#ifndef OFDM_K1Q_WPE
+#define OFDM_K1Q_WPE 1      // A/B option: amdgpu_waves_per_eu lower bound of the quad kernel
+#endif
 template <bool INV, int CONV>
-__global__ __launch_bounds__(256) void fft64_quad_kernel(const float2 *__restrict__ in, float2 *__restrict__ out,
-                                                         int64_t n) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OFDM_K1Q_WPE)))
+void fft64_quad_kernel(const float2 *__restrict__ in, float2 *__restrict__ out, int64_t n) {
     constexpr int T = OFDM_K1_QUAD_T;
     const int q = threadIdx.x & 3;
     const int r = ((q & 1) << 1) | (q >> 1);                      // output residue of this lane
@@ -266,9 +273,136 @@ __global__ __launch_bounds__(256) void fft64_quad_kernel(const float2 *__restric
 #ifdef OFDM_K1_ABL_STORE  // ablation (wrong results): every store instruction writes 512 contiguous bytes
                 out[(t0 - (threadIdx.x >> 2) + 16 * (threadIdx.x >> 6)) * 64 + 64 * pos + (threadIdx.x & 63)] = cscale(x[u][pos], out_scale);
 #else
+#if OFDM_K1_NT
+                {
+                    const float2 v = cscale(x[u][pos], out_scale);
+                    __builtin_nontemporal_store(f2v{v.x, v.y}, reinterpret_cast<f2v *>(dst + 4 * kp));
+                }
+#else
                 dst[4 * kp] = cscale(x[u][pos], out_scale);
 #endif
+#endif
             });
+        }
+    }
+}
+
+// K1 as launched by default: the quad mapping above with BOTH HBM sides coalesced through LDS (round 5;
+// VERDICT r4 item 6).  fft64_quad_kernel's lane q loads 16 B at byte 128 q + 16 c of its transform per
+// instruction, so one wave-instruction touches 64 different 128-B lines (and its stores 16 lines in 32-B pieces);
+// round 2's ablation priced perfectly coalesced loads at +9 % for fft (profiles/r02/k1q/fft_ab.txt).  Here a wave
+// owns 16 transforms (8 KB, contiguous in HBM):
+//   * loads: 8 LDS-DMA instructions (global_load_lds_dwordx4), each reading 1 KB of HBM contiguously; the lane ->
+//     chunk assignment inside each KB is permuted so that chunk j of transform t lands at slot 32 t + (j ^ s),
+//     s = 2 (t & 3) + (j >> 4): then the quad lanes' ds_read_b128 of "chunk 8 q + c" hit 16 distinct 4-bank groups
+//     in each of ds_read_b128's 16-lane groups ({0-3, 12-15, 20-27}, ...: transforms t, t + 3, t + 5, t + 6, whose
+//     (t & 3) differ) -- no bank conflicts;
+//   * the transform (DPP 4-point stage across the quad, per-lane twiddles, 16-point DIF in registers) is the quad
+//     kernel's;
+//   * stores: bin k of transform t goes to LDS float2 slot 64 t + (k ^ 4 (t & 3)) by ds_write_b64 (the 16 lanes of
+//     a 4 x 16 group write 16 distinct bank pairs), then each lane reads back 16 contiguous bytes (ds_read_b128,
+//     the XOR keeps a chunk's two bins adjacent) and writes them with one global_store_dwordx4: 1 KB contiguous per
+//     wave-instruction.
+// 32 KB of LDS per 256-thread block (5 blocks, 20 waves per CU).  In place (in == out) is safe: a wave reads all its
+// transforms before it writes them.
+#ifndef OFDM_K1_WPE
+#define OFDM_K1_WPE 4       // amdgpu_waves_per_eu lower bound: <= 128 VGPRs (95), so LDS (5 blocks per CU) sets occupancy
+#endif
+#ifndef OFDM_K1_LOAD_CPOL
+#define OFDM_K1_LOAD_CPOL 2 // cache-policy bits of the LDS-DMA loads: nt (streamed once; A/B +1.5 % on top of the above)
+#endif
+template <bool INV, int CONV>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OFDM_K1_WPE)))
+void fft64_lds_kernel(const float2 *__restrict__ in, float2 *__restrict__ out, int64_t n) {
+    __shared__ __attribute__((aligned(16))) float4 buf[4][512];       // per wave: 16 transforms x 32 chunks of 16 B
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t t_base = ((int64_t)blockIdx.x * 4 + wv) * 16;       // this wave's first transform
+    const int64_t avail = (n - t_base) * 32;                           // chunks of this wave that exist (>= 1)
+    float4 *wb = buf[wv];
+    const float4 *src = reinterpret_cast<const float4 *>(in) + t_base * 32;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int slot = 64 * i + lane, t = slot >> 5, jp = slot & 31;
+        const int j = jp ^ (2 * (t & 3) + (jp >> 4));                  // the chunk whose slot this lane fills
+        if (t * 32 + j < avail)
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src + t * 32 + j),
+                                             (__attribute__((address_space(3))) void *)(wb + 64 * i), 16, 0,
+                                             OFDM_K1_LOAD_CPOL);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                  // this wave's DMA has landed (wave-private)
+    const int q = lane & 3, tl = lane >> 2;                            // quad lane, transform within the wave
+    const int r = ((q & 1) << 1) | (q >> 1);                           // output residue of this lane
+    const int64_t t = t_base + tl;
+    const float s1 = q < 2 ? 1.0f : -1.0f;
+    const float jf = INV ? -1.0f : 1.0f;
+    const float2 ca = q == 3 ? make_float2(0.f, jf) : make_float2(q == 1 ? -1.0f : 1.0f, 0.f);
+    const float2 cb = q == 2 ? make_float2(0.f, -jf) : make_float2(1.0f, 0.f);
+    float2 tw[16];
+    static_for<1, 16>([&](auto jc) {
+        constexpr int jj = decltype(jc)::value;
+        auto w = [](auto ec) {
+            constexpr int e = decltype(ec)::value % 64;
+            return make_float2(kCos64[e], INV ? kSin64[e] : -kSin64[e]);
+        };
+        const float2 w1 = w(std::integral_constant<int, jj>{}), w2 = w(std::integral_constant<int, 2 * jj>{}),
+                     w3 = w(std::integral_constant<int, 3 * jj>{});
+        tw[jj] = r == 1 ? w1 : r == 2 ? w2 : w3;
+        if (r == 0) tw[jj] = make_float2(1.0f, 0.0f);
+    });
+    const float out_scale = INV ? ((r & 1) ? -1.0f / 64.0f : 1.0f / 64.0f) : 1.0f;
+    float2 x[64];                                                      // x[j], j < 16 used
+    {
+        typedef const __attribute__((address_space(3))) f4v lf4c;
+        const int sw = 2 * (tl & 3) + (q >> 1);                       // this lane's slot XOR
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const f4v v = *(lf4c *)(wb + 32 * tl + ((8 * q + c) ^ sw));
+            x[2 * c] = make_float2(v.x, v.y);
+            x[2 * c + 1] = make_float2(v.z, v.w);
+        }
+    }
+    static_for<0, 16>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        constexpr float sg = ((!INV || CONV == OFDM_CONV_C) && (j & 1)) ? -1.0f : 1.0f;     // (-1)^n (D5)
+        float2 v = make_float2(sg * x[j].x, sg * x[j].y);
+        const float2 p2 = dpp_f2<DPP_QUAD_XOR2>(v);
+        v = make_float2(fmaf(s1, v.x, p2.x), fmaf(s1, v.y, p2.y));
+        const float2 p1 = dpp_f2<DPP_QUAD_XOR1>(v);
+        v = make_float2(ca.x * v.x - ca.y * v.y + (cb.x * p1.x - cb.y * p1.y),
+                        ca.x * v.y + ca.y * v.x + (cb.x * p1.y + cb.y * p1.x));
+        if constexpr (j > 0) v = make_float2(fmaf(v.x, tw[j].x, -v.y * tw[j].y), fmaf(v.x, tw[j].y, v.y * tw[j].x));
+        x[j] = v;
+    });
+    dif4<INV, 16, 0>(x);                                               // bin 4 k' + r at position rev16(k')
+    {
+        typedef __attribute__((address_space(3))) f2v lf2w;
+        lf2w *ob = (lf2w *)wb + 64 * tl;
+        const int ox = 4 * (tl & 3);
+        static_for<0, 16>([&](auto pc) {
+            constexpr int pos = decltype(pc)::value;
+            constexpr int kp = ((pos & 3) << 2) | (pos >> 2);          // rev16 is its own inverse
+            const float2 v = cscale(x[pos], out_scale);
+            f2v w; w.x = v.x; w.y = v.y;
+            ob[(4 * kp + r) ^ ox] = w;
+        });
+    }
+    // every lane's bins are in LDS before any lane reads its chunks back (one wave: LDS operations complete in
+    // order; the fences keep the compiler from moving the reads above the writes)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    float4 *dst = reinterpret_cast<float4 *>(out) + t_base * 32;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int g = 64 * i + lane, tg = g >> 5, m = g & 31;
+        typedef const __attribute__((address_space(3))) f4v lf4c;
+        const f4v v = *(lf4c *)(wb + 32 * tg + (m ^ (2 * (tg & 3))));
+        if (g < avail) {
+#if OFDM_K1_NT
+            __builtin_nontemporal_store(v, reinterpret_cast<f4v *>(dst) + g);
+#else
+            dst[g] = make_float4(v.x, v.y, v.z, v.w);
+#endif
         }
     }
 }
@@ -852,9 +986,17 @@ __global__ __launch_bounds__(256, OFDM_RX_IDEAL_WAVES) void rx_ideal_kernel(RxAr
 }
 
 // ======================================================================== launchers
+#ifndef OFDM_K1_LDS
+#define OFDM_K1_LDS 1       // K1 through LDS with coalesced HBM loads and stores (fft64_lds_kernel); 0: fft64_quad_kernel
+#endif
 template <bool INV>
 static void launch_fft_conv(int conv, dim3 g, hipStream_t st, const float2 *in, float2 *out, int64_t n) {
-#if !defined(OFDM_K1_LANE) && !defined(OFDM_K1_WAVE)
+#if OFDM_K1_LDS && !defined(OFDM_K1_LANE) && !defined(OFDM_K1_WAVE)
+    const dim3 gl((unsigned)((n + 63) / 64));
+    if (conv == OFDM_CONV_C) hipLaunchKernelGGL((fft64_lds_kernel<INV, OFDM_CONV_C>), gl, dim3(256), 0, st, in, out, n);
+    else hipLaunchKernelGGL((fft64_lds_kernel<INV, OFDM_CONV_MATLAB>), gl, dim3(256), 0, st, in, out, n);
+    (void)g;
+#elif !defined(OFDM_K1_LANE) && !defined(OFDM_K1_WAVE)
     const dim3 gq((unsigned)((n + 64 * OFDM_K1_QUAD_T - 1) / (64 * OFDM_K1_QUAD_T)));
     if (conv == OFDM_CONV_C) hipLaunchKernelGGL((fft64_quad_kernel<INV, OFDM_CONV_C>), gq, dim3(256), 0, st, in, out, n);
     else hipLaunchKernelGGL((fft64_quad_kernel<INV, OFDM_CONV_MATLAB>), gq, dim3(256), 0, st, in, out, n);

@@ -103,6 +103,15 @@ class Engine:
         check(self.lib, self.lib.ofdm_fft64(self.ctx, _ptr(x), _ptr(out), n, int(inverse), abi.CONV[conv]), "fft64")
         return out
 
+    def fft64_into(self, x, out, inverse: bool = False, conv: str = "c"):
+        """fft64 into a preallocated complex64 [n, 64] device tensor (no allocation; in place allowed)."""
+        torch = _torch()
+        assert x.dtype == torch.complex64 and out.dtype == torch.complex64 and x.is_contiguous() and out.is_contiguous()
+        assert x.shape == out.shape and x.shape[-1] == 64 and x.is_cuda and out.is_cuda
+        check(self.lib, self.lib.ofdm_fft64(self.ctx, _ptr(x), _ptr(out), x.numel() // 64, int(inverse), abi.CONV[conv]),
+              "fft64")
+        return out
+
     # ---- symbol mode (the per-symbol chain) ---------------------------------------------
     def tx_buffers(self, n_frames: int):
         torch = _torch()

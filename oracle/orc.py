@@ -244,6 +244,8 @@ class RefLib:
         L.ref_packet_selection.restype = C.c_int
         L.ref_time_symbol_chain.restype = C.c_double
         L.ref_time_symbol_chain.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
+        L.ref_time_fft.restype = C.c_double
+        L.ref_time_fft.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
         self.n = L.ref_init()
 
     def waveform(self) -> np.ndarray:
@@ -272,6 +274,14 @@ class RefLib:
         i = np.ascontiguousarray(X, np.complex64); o = np.zeros_like(i)
         self.lib.ref_ifft(_p(i), _p(o), len(i))
         return o
+
+    def time_fft(self, n_transforms: int, inverse: bool = False, n_vectors: int = 1024, seed: int = 1):
+        """n_transforms calls of the reference's fft() / ifft() on 64 samples (ref_harness.c ref_time_fft) over
+        n_vectors distinct seeded inputs: (seconds, checksum)."""
+        x = np.random.default_rng(seed).standard_normal((n_vectors, 128)).astype(np.float32)
+        chk = C.c_double()
+        t = self.lib.ref_time_fft(_p(x), int(n_vectors), int(n_transforms), int(inverse), C.byref(chk))
+        return t, chk.value
 
     def channel_estimation(self, frame480: np.ndarray) -> np.ndarray:
         """Channel_Estimation (OFDM.c:830-850) on a 480-sample symbol-rate frame -> H[64]."""

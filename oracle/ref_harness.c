@@ -127,6 +127,25 @@ void ref_ifft(const float *in, float *out, int n)
     memcpy(out, y, (size_t)n * sizeof(float complex));
 }
 
+/* Time n_transforms 64-point fft() (inverse 0) or ifft() (inverse 1) calls of the reference (OFDM.c:282-339) over
+ * a buffer of distinct input vectors (CPU baseline of bench.py --workload fft64).  Returns wall seconds; *check
+ * gets a sum of the outputs (keeps the work observable). */
+double ref_time_fft(const float *in, int n_vectors, int n_transforms, int inverse, double *check)
+{
+    struct timespec t0, t1;
+    float complex x[64], y[64];
+    double acc = 0.0;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int t = 0; t < n_transforms; ++t) {
+        memcpy(x, in + (size_t)(t % n_vectors) * 128, sizeof x);   /* ifft mutates its input (OFDM.c:322) */
+        if (inverse) ifft(x, y, 64); else fft(x, y, 64);
+        acc += crealf(y[t & 63]);
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    if (check) *check = acc;
+    return (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
+}
+
 void ref_convolution(const float *in, int n, float *out)
 {
     quiet_begin();
