@@ -595,7 +595,9 @@ def main():
     # the receiver kernel this workload launches (ofdm_symbol.hip launch_rx): real-noise AWGN sweeps and
     # real-noise LS Rayleigh sweeps run the packed receiver (ofdm_rxpack.hip), the others the {E, D0, D1}
     # LS / ideal receivers
-    kernel = ("frame_sync_kernel+frame_sym_kernel" if frame_mode
+    # frames of >= 5 data symbols (captures > 4,100 samples) run the long-capture sync kernel (ofdm_frame_long.hip)
+    kernel = (("frame_sync_long_kernel+frame_sym_kernel" if args.workload == "frame8" else "frame_sync_kernel+frame_sym_kernel")
+              if frame_mode
               else "rx_pack_kernel" if kw.get("noise") == "real" and (kw.get("channel") == "awgn" or kw.get("est") == "ls")
               else ("rx_ls_kernel" if kw.get("est") == "ls" else "rx_ideal_kernel"))
     lib_id = codeobj.workload_build_id(abi.library_file(), args.workload)

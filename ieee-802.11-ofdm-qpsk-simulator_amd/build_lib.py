@@ -19,7 +19,7 @@ INCLUDE = PKG_DIR.parent / "include"
 BUILD = PKG_DIR / "_build"
 LIB = PKG_DIR / "libofdm_mi355x.so"
 SOURCES = ["ofdm_capi.hip", "ofdm_symbol.hip", "ofdm_rxpack.hip", "ofdm_rxpack_ideal.hip", "ofdm_frame.hip",
-           "ofdm_frame_sym.hip", "ofdm_frame_fix.hip"]
+           "ofdm_frame_sym.hip", "ofdm_frame_fix.hip", "ofdm_frame_long.hip"]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -fno-slp-vectorize: keep f32 math scalar (packed v_pk_* f32 gives no rate on gfx950 and its
@@ -38,7 +38,8 @@ SOURCE_FLAGS = {"ofdm_symbol.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
                 "ofdm_rxpack_ideal.hip": os.environ.get("OFDM_RXPACK_IDEAL_FLAGS", "").split(),
                 "ofdm_frame.hip": os.environ.get("OFDM_FRAME_FLAGS", "").split(),
                 "ofdm_frame_sym.hip": os.environ.get("OFDM_FRAME_SYM_FLAGS", "").split(),
-                "ofdm_frame_fix.hip": os.environ.get("OFDM_FRAME_FIX_FLAGS", "-mllvm -amdgpu-sched-strategy=max-ilp").split()}
+                "ofdm_frame_fix.hip": os.environ.get("OFDM_FRAME_FIX_FLAGS", "-mllvm -amdgpu-sched-strategy=max-ilp").split(),
+                "ofdm_frame_long.hip": os.environ.get("OFDM_FRAME_LONG_FLAGS", "").split()}
 
 
 # Kernels whose parity-dump variants (last template argument `true`) are allowed to spill: they

@@ -29,8 +29,9 @@ WORKLOAD_KERNELS = {
     "c5": ("rx_pack_kernelILi2ELi0ELi1ELb0E",),
     "c2": ("rx_pack_kernelILi0ELi0ELi0ELb0E",),
     "frame": ("frame_sync_kernelILi2ELi3008E", "frame_sym_kernelILb0ELi2E"),
-    # frame8: the generic sync kernel in both block shapes run_frame_chunk may pick (4-wave and 1-wave blocks)
-    "frame8": ("frame_sync_kernelILi0ELi0ELi4E", "frame_sync_kernelILi0ELi0ELi1E", "frame_sym_kernelILb0ELi0E"),
+    # frame8: the long-capture sync kernel (ofdm_frame_long.hip; run_frame_chunk picks it for captures > 4,100
+    # samples) and the generic symbol kernel
+    "frame8": ("frame_sync_long_kernel", "frame_sym_kernelILb0ELi0E"),
     "fft64": ("fft64_lds_kernelILb0ELi0E", "fft64_lds_kernelILb1ELi0E"),
 }
 

@@ -25,7 +25,7 @@
 
 // ofdm_frame_sym.hip / ofdm_frame_fix.hip include this file to instantiate one kernel each in a translation unit of
 // its own (their own scheduler flags, build_lib.SOURCE_FLAGS); everything else lives in this one
-#if defined(OFDM_FRAME_SYM_TU) || defined(OFDM_FRAME_FIX_TU)
+#if defined(OFDM_FRAME_SYM_TU) || defined(OFDM_FRAME_FIX_TU) || defined(OFDM_FRAME_LONG_TU)
 #define OFDM_FRAME_AUX_TU 1
 #endif
 
@@ -1348,10 +1348,363 @@ void launch_frame_fix(hipStream_t st, const FrameArgs &a, dim3 grid, size_t lds)
     hipLaunchKernelGGL((frame_sync_kernel<2, 3008>), grid, dim3(SYNC_THREADS), lds, st, a);
 }
 }  // namespace ofdm
+#elif defined(OFDM_FRAME_LONG_TU)
+// ---------------------------------------------------------------- K4b for long captures
+// Frames of 5..8 data symbols (ofdm_set_message) give captures of 4,482..5,955 samples: 18-24 KB of real parts per
+// wave, so frame_sync_kernel<0, 0> fits one four-wave block per CU (1 wave per SIMD).  This kernel keeps at most
+// LW_RES = 4,016 capture samples resident per wave (16 KB; two blocks, 2 waves per SIMD) by detecting in rounds
+// of 64 lanes x 31 positions (LW_ROUND = 1,984 positions, 2,031 samples each) and generating the capture in two
+// pieces, both from the same counter-based Philox stream as the whole capture:
+//   1. (three rounds only) samples [2 LW_ROUND, L) -> round 2 (positions [3,968, Lc));
+//   2. samples [0, min(L, LW_RES)) -> rounds 0 and 1 (the piece the matched filter almost always reads: the
+//      selected packet starts in the first frame period);
+//   3. when the matched filter's samples [p - 20, p + 2 (nfr - 1) + 10] leave the resident piece (the first
+//      valid front lies past ~2,070, ~9 % of 8-symbol trials), they are generated again into the region.
+// The filtered frame fr[] then overwrites the region: a lane holds its runs' outputs in registers until every
+// lane's reads are done.  Packet detection / selection, the matched filter, CFO and hand-off are the generic
+// kernel's arithmetic, so every counter and packet_idx equals frame_sync_kernel<0, 0>'s
+// (tests/test_gpu_frame.py::test_long_capture_kernel_equals_generic).  Sweeps only (generated captures, no
+// dumps, no word-length statistics); no lazy capture (for long frames round 0 never decides: two fronts are one
+// frame period, >= 1,940 positions, apart).
+constexpr int LW_CHUNK = 31;
+constexpr int LW_ROUND = 64 * LW_CHUNK;              // 1,984 positions per round
+constexpr int LW_RES = 2 * LW_ROUND + 48;             // resident capture samples (rounds 0 and 1 and their windows)
+constexpr int LW_MAXP = 3;                            // matched-filter passes of 64 runs (33 + 13 nd <= 137 runs)
+#ifndef FRAME_LONG_MINW
+#define FRAME_LONG_MINW 2
+#endif
+#ifndef FRAME_MF_B64_LONG
+#define FRAME_MF_B64_LONG FRAME_MF_B64_GEN   // lds_readn form of the long kernel's matched filter
+#endif
+template <int W>
+__global__ __launch_bounds__(64 * W, FRAME_LONG_MINW) void frame_sync_long_kernel(FrameArgs a) {
+    constexpr int SYNC_WAVES_L = W, SYNC_THREADS_L = 64 * W;
+    extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
+    const int L = a.cap_len, Lc = L - 47;
+    const int nfr = fr_len(a.n_data);
+    constexpr int ns = 2;
+    unsigned long long *acc = smem;                                           // [n_snr][2]
+    float *imt = reinterpret_cast<float *>(acc + a.n_snr * ns);
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float *rbase = imt + ((a.imt_len + 3) & ~3) + wv * a.region_floats;
+    for (int i = threadIdx.x; i < a.n_snr * ns; i += SYNC_THREADS_L) acc[i] = 0ull;
+    for (int k = threadIdx.x; k < a.imt_len; k += SYNC_THREADS_L) imt[k] = a.wave[k % a.im_period].y;
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int R = (Lc + LW_ROUND - 1) / LW_ROUND;                            // 2 or 3 rounds (host-checked)
+    const int nwaves = (int)gridDim.x * SYNC_WAVES_L;
+    int64_t run_end = ((int64_t)blockIdx.x * SYNC_WAVES_L + wv) * FRAME_ITEM_RUN + FRAME_ITEM_RUN;
+    int nxt = 0;
+    for (int64_t i = run_end - FRAME_ITEM_RUN; i < a.n_items;) {
+        using KArgs = const __attribute__((address_space(4))) FrameArgs;
+        KArgs *ap = (KArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(ap));
+        KArgs &a = *ap;
+        const int n_data = a.n_data, wave_len = a.wave_len;
+        const ImMod im_mod{a.im_period, a.im_magic};
+        if (lane == 0 && i == run_end - FRAME_ITEM_RUN) nxt = nwaves + (int)atomicAdd(a.work, 1ull);
+        uint32_t qr;
+        const int64_t ti = a.trial0 + snr_divmod((uint32_t)a.q0 + (uint32_t)i, (uint32_t)a.n_snr, a.snr_magic, qr);
+        const int q = (int)qr;
+        const uint64_t t = a.first_trial + (uint64_t)ti;
+        const uint32_t t_lo = (uint32_t)t, t_hi = (uint32_t)(t >> 32), qs = (uint32_t)(a.q_base + q);
+        const float sigma = a.sigma[q];
+        int rx_start = a.fixed_start;
+        if (rx_start < 0) {
+            const uint4 o = philox10(t_lo, t_hi, 0u, STREAM_START | qs, a.k0, a.k1);
+            rx_start = (int)(o.x % (uint32_t)(wave_len - L));
+        }
+        rx_start = __builtin_amdgcn_readfirstlane(rx_start);
+        const int off = rx_start & 3, b0 = rx_start >> 2;
+        const float *r = rbase + off;                        // r[n] = Re capture sample n of the resident piece
+        const int im0 = im_mod(rx_start);
+        int lx = lane;
+        opaque(lx);
+        // ---- Packet_Detection (OFDM.c:659-683) in rounds of LW_ROUND positions, lane l of round rho owning
+        // [rho LW_ROUND + 31 l, +31) -- frame_sync_kernel's sliding sums and sign-bit crossings; rp: this round's
+        // view of the capture (sample n at rp[n]) ----
+        unsigned long long cm[3] = {0ull, 0ull, 0ull};
+        int first[3] = {-1, -1, -1}, last[3] = {-1, -1, -1};
+        auto detect = [&](auto rc, const float *rp) {
+            constexpr int rho = decltype(rc)::value;
+            const int n0 = rho * LW_ROUND + lx * LW_CHUNK, n1 = min(n0 + LW_CHUNK, Lc);
+            unsigned long long cmask = 0ull;
+            if (n0 < n1) {
+                using LdsF = const __attribute__((address_space(3))) float;
+                LdsF *ti_ = (LdsF *)(imt + im_mod(im0 + n0));
+                LdsF *tr_ = (LdsF *)(rp + n0);
+                opaque(ti_);
+                opaque(tr_);
+                float sx = 0.f, sy = 0.f, pw = 0.f;
+                uint32_t mlo = 0u, mhi = 0u;
+                constexpr int nbat = (LW_CHUNK + DET_B - 1) / DET_B;
+                float xr[nbat + 3][DET_B], xi[nbat + 3][DET_B];
+                auto load_blk = [&](auto jc) {
+                    constexpr int j = decltype(jc)::value;
+#pragma unroll
+                    for (int k = 0; k < DET_B; ++k) { xr[j][k] = tr_[DET_B * j + k]; xi[j][k] = ti_[DET_B * j + k]; }
+                };
+                load_blk(std::integral_constant<int, 0>{});
+                load_blk(std::integral_constant<int, 1>{});
+                load_blk(std::integral_constant<int, 2>{});
+                static_for<0, 2>([&](auto hc) {
+                    constexpr int h = decltype(hc)::value;
+#pragma unroll
+                    for (int kk = 0; kk < DET_B; ++kk) {
+                        const float ux = xr[h][kk], uy = xi[h][kk], vx = xr[h + 1][kk], vy = xi[h + 1][kk];
+                        sx = fmaf(ux, vx, sx); sx = fmaf(-uy, vy, sx);
+                        sy = fmaf(ux, vy, sy); sy = fmaf(uy, vx, sy);
+                        pw = fmaf(vx, vx, pw); pw = fmaf(vy, vy, pw);
+                    }
+                });
+                static_for<0, nbat>([&](auto bc) {
+                    constexpr int b = decltype(bc)::value;
+                    load_blk(std::integral_constant<int, b + 3>{});
+#pragma unroll
+                    for (int k = 0; k < DET_B; ++k) {
+                        const float o0x = xr[b][k], o0y = xi[b][k], o1x = xr[b + 1][k], o1y = xi[b + 1][k];
+                        const float i0x = xr[b + 2][k], i0y = xi[b + 2][k], i1x = xr[b + 3][k], i1y = xi[b + 3][k];
+                        const float num = fmaf(sx, sx, sy * sy), h = 0.75f * pw;
+                        const float tt = fmaf(h, pw, -num);
+                        mhi = __builtin_amdgcn_alignbit(mhi, mlo, 31);
+                        mlo = __builtin_amdgcn_alignbit(mlo, __float_as_uint(tt), 31);
+                        sx = fmaf(i0x, i1x, sx); sx = fmaf(-i0y, i1y, sx);
+                        sx = fmaf(-o0x, o1x, sx); sx = fmaf(o0y, o1y, sx);
+                        sy = fmaf(i0x, i1y, sy); sy = fmaf(i0y, i1x, sy);
+                        sy = fmaf(-o0x, o1y, sy); sy = fmaf(-o0y, o1x, sy);
+                        pw = fmaf(i1x, i1x, pw); pw = fmaf(i1y, i1y, pw);
+                        pw = fmaf(-o1x, o1x, pw); pw = fmaf(-o1y, o1y, pw);
+                    }
+                });
+                constexpr int J = nbat * DET_B;
+                const unsigned long long rev = ((unsigned long long)__builtin_bitreverse32(mlo) << 32) |
+                                               __builtin_bitreverse32(mhi);
+                cmask = rev >> (64 - J);
+                cmask &= (1ull << (n1 - n0)) - 1ull;
+            }
+            cm[rho] = cmask;
+            first[rho] = cmask ? n0 + __builtin_ctzll(cmask) : -1;
+            last[rho] = cmask ? n0 + 63 - __builtin_clzll(cmask) : -1;
+        };
+        // piece 1 (three rounds): samples [2 LW_ROUND, L) at region float off + n - LW_ROUND, round 2
+        if (R == 3) {
+            capture_blocks(a, wave_len, rbase, b0 + LW_ROUND / 4, (rx_start + 2 * LW_ROUND) >> 2, (rx_start + L - 1) >> 2,
+                           lane, t_lo, t_hi, qs, sigma);
+            wave_lds_sync();
+            detect(std::integral_constant<int, 2>{}, r - LW_ROUND);
+            wave_lds_sync();                                  // every lane's loads are done: piece 2 overwrites
+        }
+        // piece 2: samples [0, min(L, LW_RES)), rounds 0 and 1
+        const int res_end = min(L, LW_RES);
+        capture_blocks(a, wave_len, rbase, b0, b0, (rx_start + res_end - 1) >> 2, lane, t_lo, t_hi, qs, sigma);
+        wave_lds_sync();
+        detect(std::integral_constant<int, 0>{}, r);
+        detect(std::integral_constant<int, 1>{}, r);
+        // the crossing bit of position pos (< Lc) from the lane that owns it (ds_bpermute)
+        auto crossing = [&](int pos) {
+            const int rd = pos / LW_ROUND, rel = pos - rd * LW_ROUND;
+            const int owner = rel / LW_CHUNK, bit = rel - owner * LW_CHUNK;
+            unsigned long long w = 0ull;
+            static_for<0, 3>([&](auto r2c) {
+                constexpr int r2 = decltype(r2c)::value;
+                if (r2 < R) {
+                    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)cm[r2], owner, 64);
+                    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(cm[r2] >> 32), owner, 64);
+                    if (rd == r2) w = ((unsigned long long)hi << 32) | lo;
+                }
+            });
+            return ((w >> bit) & 1ull) != 0ull;
+        };
+        // ---- Packet_Selection (OFDM.c:685-771) over the R rounds (frame_sync_kernel's rule) ----
+        int vmin = 0x7fffffff, fmax_ = -1, carry = -1;
+        static_for<0, 3>([&](auto rc) {
+            constexpr int rho = decltype(rc)::value;
+            if (rho < R) {
+                const int pm = max(wave_prefix_max(last[rho]), carry);
+                const int prev = max(wave_shr1(pm), carry);
+                const int front = (first[rho] >= 0 && first[rho] - prev > 300) ? first[rho] : -1;
+                carry = __builtin_amdgcn_readlane(pm, 63);
+                const int pos = front + 230;
+                const bool valid = crossing(pos < Lc ? pos : 0) && front >= 0 && pos < Lc;
+                vmin = min(vmin, valid ? front : 0x7fffffff);
+                fmax_ = max(fmax_, front);
+            }
+        });
+        const int cmin = wave_min_i(vmin), cmax = wave_max_i(fmax_);
+        const int cand = cmin < cmax ? cmin : 0x7fffffff;
+        const bool sync_fail = cand == 0x7fffffff;
+        const int p = sync_fail ? 0 : cand + 10 + 1;
+        // ---- the matched filter's samples [p - 20, p + 2 (nfr - 1) + 10]: resident, or generated again ----
+        const float *rm = r;
+        {
+            const int lo = max(p - 20, 0), hi = min(p + 2 * (nfr - 1) + 10, L - 1);
+            if (hi >= res_end) {
+                const int s0 = lo & ~3;
+                wave_lds_sync();                              // detection's loads are done
+                capture_blocks(a, wave_len, rbase, (rx_start + s0) >> 2, (rx_start + s0) >> 2, (rx_start + hi) >> 2, lane,
+                               t_lo, t_hi, qs, sigma);
+                wave_lds_sync();
+                rm = r - s0;                                  // sample n at rbase + off + n - s0
+            }
+        }
+        // ---- RRC matched filter at the needed instants (frame_sync_kernel's runs), outputs held in registers ----
+        bool oob_l = false;
+        float tv[11];
+        {
+            using kchar = __attribute__((address_space(4))) char;
+            using kfloat = __attribute__((address_space(4))) float;
+            const kfloat *tp = (const kfloat *)((const kchar *)__builtin_amdgcn_kernarg_segment_ptr() +
+                                                offsetof(FrameArgs, taps));
+            asm volatile("" : "+s"(tp));
+#pragma unroll
+            for (int j = 0; j < 11; ++j) asm volatile("v_mov_b32 %0, %1" : "=v"(tv[j]) : "s"(tp[j]));
+        }
+        const int offm = (int)(rm - rbase);                   // float offset of sample 0 in the region (may be < 0)
+        const int par_r = (offm + p) & 1, par_i = (im0 + p) & 1;
+        constexpr int MF_RUN = 5, MF_W = 2 * MF_RUN + 19;
+        constexpr int c0r = (32 + MF_RUN - 1) / MF_RUN, c1r = c0r + (128 + MF_RUN - 1) / MF_RUN;
+        constexpr int cd = (64 + MF_RUN - 1) / MF_RUN;
+        const int n_runs = c1r + cd * n_data;
+        float2 mfo[LW_MAXP][MF_RUN];
+        int mfs[LW_MAXP], mfe[LW_MAXP];
+        static_for<0, LW_MAXP>([&](auto pc) {
+            constexpr int pi = decltype(pc)::value;
+            const int u = lx + 64 * pi;
+            int s0 = 0, e = 0;
+            if (u < n_runs) {
+                if (u < c0r) {
+                    s0 = 80 + MF_RUN * u; e = 112;
+                } else if (u < c1r) {
+                    s0 = 192 + MF_RUN * (u - c0r); e = 320;
+                } else {
+                    const int d = (u - c1r) / cd, k = u - c1r - d * cd;
+                    s0 = 336 + 80 * d + MF_RUN * k; e = 400 + 80 * d;
+                }
+                e = min(e, s0 + MF_RUN);
+            }
+            mfs[pi] = s0;
+            mfe[pi] = e;
+            const int n_lo = p + 2 * s0 - 20;
+            if (u < n_runs && n_lo >= 0 && p + 2 * (e - 1) < L) {
+                float xr[MF_W], xi[MF_W];
+                const int si = im_mod(im0 + n_lo);
+                if (par_r) lds_readn<1, FRAME_MF_B64_LONG>(rm, n_lo, xr); else lds_readn<0, FRAME_MF_B64_LONG>(rm, n_lo, xr);
+                if (par_i) lds_readn<1, FRAME_MF_B64_LONG>(imt, si, xi); else lds_readn<0, FRAME_MF_B64_LONG>(imt, si, xi);
+#pragma unroll
+                for (int o = 0; o < MF_RUN; ++o) {
+                    float2 v = make_float2(xr[2 * o + 10] * tv[10], xi[2 * o + 10] * tv[10]);
+#pragma unroll
+                    for (int tt = 0; tt < 10; ++tt) {
+                        v.x = fmaf(xr[2 * o + 20 - tt] + xr[2 * o + tt], tv[tt], v.x);
+                        v.y = fmaf(xi[2 * o + 20 - tt] + xi[2 * o + tt], tv[tt], v.y);
+                    }
+                    mfo[pi][o] = v;
+                }
+            } else {
+#pragma unroll
+                for (int o = 0; o < MF_RUN; ++o) {           // the per-instant path (windows leaving the capture)
+                    const int n = p + 2 * (s0 + o);
+                    float2 v = make_float2(0.f, 0.f);
+                    if (u < n_runs && s0 + o < e) {
+                        if (n >= L + 20) {
+                            oob_l = true;
+                        } else {
+                            for (int tt = 0; tt < 21; ++tt) {
+                                const int m = n - tt;
+                                const int mc = min(max(m, 0), L - 1);
+                                const bool in = m >= 0 && m < L;
+                                const float xr = in ? rm[mc] : 0.f, xi = in ? imt[im_mod(im0 + mc)] : 0.f;
+                                const float h = tv[tt <= 10 ? tt : 20 - tt];
+                                v.x = fmaf(xr, h, v.x);
+                                v.y = fmaf(xi, h, v.y);
+                            }
+                        }
+                    }
+                    mfo[pi][o] = v;
+                }
+            }
+        });
+        const bool oob = __ballot(oob_l) != 0ull;
+        wave_lds_sync();                                      // every lane's capture reads are done
+        float2 *fr = reinterpret_cast<float2 *>(rbase);       // fr[] overwrites the region
+        static_for<0, LW_MAXP>([&](auto pc) {
+            constexpr int pi = decltype(pc)::value;
+#pragma unroll
+            for (int o = 0; o < MF_RUN; ++o)
+                if (mfs[pi] + o < mfe[pi]) fr[mfs[pi] + o] = mfo[pi][o];
+        });
+        wave_lds_sync();
+        // ---- coarse / fine CFO and the hand-off (frame_sync_kernel's generic path) ----
+        const float2 cu = fr[80 + (lx & 15)], cw = fr[96 + (lx & 15)], l1 = fr[192 + lx], l2 = fr[256 + lx];
+        float2 pp = make_float2(0.f, 0.f);
+        if (lx < 16) pp = make_float2(cu.x * cw.x + cu.y * cw.y, cu.y * cw.x - cu.x * cw.y);
+        pp.x = wave_sum_f(pp.x);
+        pp.y = wave_sum_f(pp.y);
+        double fc = (-1.0 / (2.0 * M_PI * 16.0 * TS)) * (double)atan2_cfo(pp.y, pp.x);
+        if (a.float_cfo) fc = (double)(float)fc;
+        {
+            const float2 u = cfo_rot(l1, fc * TS, 192 + lx), w = cfo_rot(l2, fc * TS, 256 + lx);
+            pp = make_float2(u.x * w.x + u.y * w.y, u.y * w.x - u.x * w.y);
+        }
+        pp.x = wave_sum_f(pp.x);
+        pp.y = wave_sum_f(pp.y);
+        double ff = (-1.0 / (2.0 * M_PI * 64.0 * TS)) * (double)atan2_cfo(pp.y, pp.x);
+        if (a.float_cfo) ff = (double)(float)ff;
+        const int nw = 1 + n_data;
+        float2 *dst = win_item(a.win, a.ipb, nw, i);
+        const double fcf_ts = (fc + ff) * TS;
+        const uint32_t inv_nw = (65536u + (uint32_t)nw - 1u) / (uint32_t)nw;
+        for (int j = lx; j < 64 * nw; j += 64) {
+            const int n = (int)(((uint32_t)j * inv_nw) >> 16), w = j - n * nw;
+            float2 v;
+            if (w == 0) {
+                const float2 u = cfo_rot(fr[192 + n], fcf_ts, 192 + n), x = cfo_rot(fr[256 + n], fcf_ts, 256 + n);
+                v = make_float2(u.x + x.x, u.y + x.y);
+            } else {
+                const int k = 336 + 80 * (w - 1) + n;
+                v = cfo_rot(fr[k], fcf_ts, k);
+            }
+            dst[win_off(n, a.ipb, nw) + w] = v;
+        }
+        if (lx == 0) {
+            a.info[i] = make_int4(p, sync_fail, oob, rx_start);
+            if (sync_fail) atomicAdd(&acc[q * ns + 0], 1ull);
+            if (oob) atomicAdd(&acc[q * ns + 1], 1ull);
+            if (a.pidx_out) a.pidx_out[(int64_t)q * a.n_trials + ti] = p;
+        }
+        if (i + 1 < run_end) {
+            ++i;
+        } else {
+            i = (int64_t)__builtin_amdgcn_readfirstlane(nxt) * FRAME_ITEM_RUN;
+            run_end = i + FRAME_ITEM_RUN;
+        }
+        wave_lds_sync();                                      // the next capture overwrites this item's region
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < a.n_snr; k += SYNC_THREADS_L) {
+        unsigned long long *c = a.counters + k * OFDM_NCOUNTERS;
+        const unsigned long long *sl = acc + k * ns;
+        if (sl[0]) atomicAdd(&c[OFDM_C_SYNC_FAIL], sl[0]);
+        if (sl[1]) atomicAdd(&c[OFDM_C_OOB], sl[1]);
+    }
+}
+
+// launcher and occupancy handle (ofdm_frame_long.hip)
+const void *frame_long_kernel() { return reinterpret_cast<const void *>(&frame_sync_long_kernel<SYNC_WAVES>); }
+void launch_frame_long(hipStream_t st, const FrameArgs &a, dim3 grid, size_t lds) {
+    hipLaunchKernelGGL((frame_sync_long_kernel<SYNC_WAVES>), grid, dim3(SYNC_THREADS), lds, st, a);
+}
+}  // namespace ofdm
 #else
 void launch_frame_sym(hipStream_t st, const FrameArgs &a, int cus);     // ofdm_frame_sym.hip
 const void *frame_fix_kernel();                                         // ofdm_frame_fix.hip
 void launch_frame_fix(hipStream_t st, const FrameArgs &a, dim3 grid, size_t lds);
+const void *frame_long_kernel();                                        // ofdm_frame_long.hip
+void launch_frame_long(hipStream_t st, const FrameArgs &a, dim3 grid, size_t lds);
+// the long-capture kernel's per-wave region (floats): the resident piece (LW_RES samples + capture offset + the last
+// detection lane's block overshoot), which also holds a regenerated matched-filter window and then fr[]
+constexpr int FRAME_LONG_REGION = 4032;
+constexpr int FRAME_LONG_MIN_CAP = 4100;     // captures longer than this (frames of >= 5 data symbols) run it
 
 // ======================================================================== host side
 // rcosdesign(0.5, 10, 2, 'sqrt') (Tester.m:112; OFDM.c:32 holds the same values as floats)
@@ -1502,6 +1855,22 @@ static int run_frame_chunk(Ctx *c, FrameArgs &a) {
     // statistics) runs the instantiation with that geometry folded in; OFDM_FRAME_GENERIC=1 forces the generic
     // one (the equivalence test)
     const int64_t runs = (a.n_items + FRAME_ITEM_RUN - 1) / FRAME_ITEM_RUN;
+    // long captures (frames of >= 5 data symbols): frame_sync_long_kernel keeps two capture pieces per wave, not
+    // the whole capture (2 waves per SIMD instead of 1); sweeps only.  OFDM_FRAME_NO_LONG=1 forces the generic kernel
+    // (the equivalence test)
+    const bool is_long = a.cap_len > FRAME_LONG_MIN_CAP && a.cap_len - 47 <= 3 * 64 * 31 && !a.ext && !a.dbg_res &&
+                         !a.dbg_ints && !a.dbg_bits && !a.dbg_eq && !a.dbg_corr && !a.dbg_frame && !a.word_stats &&
+                         2 * fr_len(a.n_data) + 40 <= FRAME_LONG_REGION && !getenv("OFDM_FRAME_NO_LONG");
+    if (is_long) {
+        a.region_floats = FRAME_LONG_REGION;
+        const size_t lds_l = (size_t)a.n_snr * 2 * 8 + (((size_t)a.imt_len * 4 + 15) & ~size_t(15)) +
+                             (size_t)SYNC_WAVES * FRAME_LONG_REGION * 4;
+        const dim3 gl(occupancy_grid(frame_long_kernel(), SYNC_THREADS, lds_l, c->cus, (runs + SYNC_WAVES - 1) / SYNC_WAVES, 1));
+        launch_frame_long(c->stream, a, gl, lds_l);
+        launch_frame_sym(c->stream, a, c->cus);
+        HIPOK(hipGetLastError());
+        return OFDM_OK;
+    }
     const bool fixed = a.n_data == 2 && a.cap_len == cap_len_for(2) && a.wave_len == wave_len_for(2) && !a.ext &&
                        !a.dbg_res && !a.dbg_ints && !a.dbg_bits && !a.dbg_eq && !a.dbg_corr && !a.dbg_frame &&
                        !a.word_stats && !getenv("OFDM_FRAME_GENERIC");

@@ -23,8 +23,8 @@ sys.path.insert(0, str(ROOT / "tools"))
 from isa_mix import COST  # noqa: E402
 from pmc_summary import kernel_key  # noqa: E402
 
-SETS = {"frame": ("frame_sync_kernel", "frame_sym_kernel"), "c3": ("rx_pack_kernel",), "c5": ("rx_pack_kernel",),
-        "c2": ("rx_pack_kernel",)}
+SETS = {"frame": ("frame_sync_kernel", "frame_sym_kernel"), "frame8": ("frame_sync_long_kernel", "frame_sym_kernel"),
+        "c3": ("rx_pack_kernel",), "c5": ("rx_pack_kernel",), "c2": ("rx_pack_kernel",)}
 
 
 def counters(dirs, kernels):

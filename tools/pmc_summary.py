@@ -22,10 +22,10 @@ from collections import defaultdict
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-KERNELS = ("rx_pack_kernel", "rx_ls_kernel", "rx_ideal_kernel", "tx_symbols_kernel", "frame_sync_kernel",
-           "frame_sym_kernel", "fft64_lds_kernel")
-RX_SETS = (("rx_pack_kernel",), ("rx_ls_kernel",), ("rx_ideal_kernel",), ("frame_sync_kernel", "frame_sym_kernel"),
-           ("fft64_lds_kernel",))
+KERNELS = ("rx_pack_kernel", "rx_ls_kernel", "rx_ideal_kernel", "tx_symbols_kernel", "frame_sync_long_kernel",
+           "frame_sync_kernel", "frame_sym_kernel", "fft64_lds_kernel")
+RX_SETS = (("rx_pack_kernel",), ("rx_ls_kernel",), ("rx_ideal_kernel",), ("frame_sync_long_kernel", "frame_sym_kernel"),
+           ("frame_sync_kernel", "frame_sym_kernel"), ("fft64_lds_kernel",))
 CUS, SIMDS, XCDS = 256, 4, 8
 NOMINAL_CLOCK = 2.4e9
 
