@@ -82,6 +82,13 @@ def main(argv):
            "dispatches_per_launch": per_launch,
            "trace_avg_launch_ms": avg_s * 1e3, "line_avg_launch_ms": rf["avg_launch_ms"],
            "line_frac": rf.get("frac")}
+    if rf.get("bound") == "hbm":     # fft64: algorithmic bytes per unit against the HBM peak (GB/s)
+        bpu = rf["algorithmic_bytes_per_unit"]
+        out["bytes_per_unit"] = bpu
+        out["trace_frac"] = upl * bpu / avg_s / 1e9 / rf["peak"]
+        out["line_events_frac"] = upl * bpu / (rf["avg_launch_ms"] * 1e-3) / 1e9 / rf["peak"]
+        out["frac_rel_diff"] = out["trace_frac"] / out["line_events_frac"] - 1
+        ipu = None
     if ipu:
         out["instr_per_unit"], out["pmc_source"] = ipu, pmc_src
         out["trace_frac"] = upl * ipu / avg_s / rf["peak"]
