@@ -77,6 +77,7 @@ WORKLOADS = {
               "launch", {}, 1 << 24, "weak"),
 }
 FFT_BYTES_PER_TRANSFORM = 1024     # 64 complex f32 read + 64 written
+STEP_DEFAULTS = {"c2": (50, 10)}   # (steps, warmup) when not given
 # data symbols per frame (trial) of each workload; frame8 sets its message before the sweep
 FRAME_DATA = {"frame8": 8}
 FRAME8_MESSAGE = (b"The quick brown fox jumps over the lazy dog; 802.11a OFDM-QPSK frames on MI355X, eight symbols.. ")[:96]
@@ -489,8 +490,8 @@ def wants_cpu_baseline(args) -> bool:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default: 5; c2 50)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed warm-up steps (default: 2; c2 10)")
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
     ap.add_argument("--symbols", type=int, default=0,
                     help="override data symbols per SNR point (per GPU for weak workloads, total for strong)")
@@ -500,6 +501,11 @@ def main():
     ap.add_argument("--pipeline", choices=("auto", "fused", "streams"), default="auto",
                     help="next chunk's Tx: fused into the LS receiver (auto for real-noise LS) or a second stream")
     args = ap.parse_args()
+    # c2's step is one ~1 ms launch: 5 steps would time mostly the clock ramp (1.94 GHz in the first launches, 2.36 in
+    # the last), so its defaults are longer; every other workload's step is >= 6 ms
+    dflt = STEP_DEFAULTS.get(args.workload, (5, 2))
+    args.steps = dflt[0] if args.steps is None else args.steps
+    args.warmup = dflt[1] if args.warmup is None else args.warmup
 
     # host-side reference timing first, before anything touches the GPU (worker processes are spawned).
     # Under torchrun rank 0 (local rank 0 of the one node) times it before forming the process group; the

@@ -130,6 +130,7 @@ def test_lazy_capture_equals_full_evaluation(engine, pkg, monkeypatch):
     assert np.mean(lp[8:] > 0) > 0.99                         # >= 16 dB: nearly every trial synchronises
     monkeypatch.delenv("OFDM_FRAME_NO_LAZY")
     msg = (b"lazy capture, eight data symbols. " * 3)[:96]
+    monkeypatch.setenv("OFDM_FRAME_NO_LONG", "1")     # the generic kernel's lazy path (the long kernel has none)
     with pkg.Engine(0) as e8:
         assert e8.set_message(msg) == 8
         cfg8 = pkg.make_cfg(payload="message")
@@ -159,11 +160,13 @@ def test_fixed_geometry_kernel_equals_generic(engine, pkg, monkeypatch, no_lazy)
 
 
 def test_long_message_one_wave_blocks_equal_four_wave_blocks(pkg, monkeypatch):
-    """An 8-symbol message's 5955-sample captures take 24 KB of LDS per wave: one four-wave block fits per CU,
-    five one-wave blocks would (measured slower, see run_frame_chunk).  The one-wave instantiation
-    (OFDM_FRAME_BLOCK1=1) gives every counter and packet_idx of the four-wave one."""
+    """An 8-symbol message's 5955-sample captures take 24 KB of LDS per wave in the generic sync kernel: one
+    four-wave block fits per CU, five one-wave blocks would (measured slower, see run_frame_chunk).  The
+    one-wave instantiation (OFDM_FRAME_BLOCK1=1) gives every counter and packet_idx of the four-wave one (both with
+    the long-capture kernel switched off, OFDM_FRAME_NO_LONG=1)."""
     snrs = np.array([4.0, 10.0, 16.0, 30.0])
     msg = (b"one-wave blocks for long messages " * 3)[:96]
+    monkeypatch.setenv("OFDM_FRAME_NO_LONG", "1")
     with pkg.Engine(0) as e8:
         assert e8.set_message(msg) == 8
         cfg8 = pkg.make_cfg(payload="message")
@@ -173,6 +176,30 @@ def test_long_message_one_wave_blocks_equal_four_wave_blocks(pkg, monkeypatch):
     assert np.array_equal(p1, p4)
     assert np.array_equal(one, four)
     assert np.mean(p1[2:] > 0) > 0.99
+
+
+@pytest.mark.parametrize("msg_len", [96, 80, 49])
+def test_long_capture_kernel_equals_generic(pkg, monkeypatch, msg_len):
+    """Frames of >= 5 data symbols (captures > 4,100 samples) run frame_sync_long_kernel: two resident capture
+    pieces per wave (the last detection round's samples, then [0, 4,016)), the matched-filter window generated again
+    when it leaves the resident piece, fr[] over the region.  Every counter and packet_idx equals the generic
+    kernel's (OFDM_FRAME_NO_LONG=1), over the bench's SNR grid, for 8-, 7- and 5-symbol messages (two rounds of
+    detection for the 5-symbol 4,482-sample captures, three for the others).  Chunked long sweeps (chunk starts off
+    the SNR grid) are test_frame_sweep_nomem_halving_and_nonzero_q0[message8]."""
+    snrs = np.arange(0.0, 31.0, 2.0)
+    msg = (b"The long-capture kernel keeps two pieces of the capture resident per wave. " * 2)[:msg_len]
+    with pkg.Engine(0) as e:
+        nd = e.set_message(msg)
+        assert nd == -(-8 * msg_len // 96) and nd >= 5
+        cfg = pkg.make_cfg(payload="message")
+        lng, lp = e.frame_sweep(cfg, snrs, 1500, want_packet_idx=True, first_trial=3)
+        monkeypatch.setenv("OFDM_FRAME_NO_LONG", "1")
+        gen, gp = e.frame_sweep(cfg, snrs, 1500, want_packet_idx=True, first_trial=3)
+        monkeypatch.delenv("OFDM_FRAME_NO_LONG")
+    assert np.array_equal(lp, gp)
+    assert np.array_equal(lng, gen)
+    assert lng[0, 0] == 1500 and np.mean(lp[-4:] > 0) > 0.99       # high SNR: nearly every trial synchronises
+    assert lng[-1, 3] == 0                                           # 30 dB: error-free
 
 
 def test_frame_sweep_two_chunks_equal_their_halves(engine, pkg):
