@@ -107,6 +107,14 @@ def issue_cap(pmc: dict, frac: float) -> dict:
                 "issue_model_note": "cap = 2 x VALU / SIMD cycles of the dynamic class mix (PMC class counters) at "
                                     "%d waves/SIMD, unclassified instructions priced slow (cap) or fast (upper end)"
                                     % m["waves_per_simd"]}
+    if m.get("method") == "dynamic_split":   # tools/mix_cap.py --split-from: a point estimate inside that range
+        lo, hi = m["cap_frac_range"]
+        return {"issue_model_cap_frac": m["cap_frac"], "issue_model_cap_frac_range": [lo, hi],
+                "frac_of_issue_model_cap": frac / m["cap_frac"], "frac_of_issue_model_cap_range": [frac / hi, frac / lo],
+                "issue_model_note": "cap = 2 x VALU / SIMD cycles of the dynamic class mix (PMC class counters) at "
+                                    "%d waves/SIMD, the unclassified instructions split fast / slow / cndmask as in "
+                                    "the classified model of frame's sync kernel (%s); range: all slow .. all fast"
+                                    % (m["waves_per_simd"], m["split_source"])}
     if m.get("method") == "classified":  # tools/frame_mix.py: every VALU instruction classified, blocks weighted
         return {"issue_model_cap_frac": m["cap_frac"], "frac_of_issue_model_cap": frac / m["cap_frac"],
                 "issue_model_note": "cap = 2 x VALU / class-priced SIMD cycles at %d waves/SIMD of both kernels' "

@@ -1816,7 +1816,8 @@ static int32_t word_bits(double mn, double mx) {
 #endif
 constexpr int64_t FRAME_CHUNK_ITEMS = int64_t(1) << FRAME_CHUNK_LOG2;
 // items per chunk for n_data data symbols: 2^22, capped so that the hand-off buffer holds no more windows than the
-// reference message's 2^22 items do (8 GiB; ADVICE r3: 8-symbol messages would otherwise take 21 GB)
+// reference message's 2^22 items do (1 + n_data windows of 512 B per item: 6 GiB; ADVICE r3: 8-symbol messages
+// would otherwise take 19 GiB)
 static int64_t frame_chunk_items(int n_data) {
     return std::min<int64_t>(FRAME_CHUNK_ITEMS, FRAME_CHUNK_ITEMS * 3 / (1 + n_data));
 }

@@ -151,6 +151,20 @@ def test_dynamic_mix_cap(tmp_path):
     cap = b.issue_cap({"issue_model": {"method": "dynamic", "cap_frac": lo, "cap_frac_range": [lo, hi],
                                        "waves_per_simd": 3}}, 0.5)
     assert cap["frac_of_issue_model_cap_range"] == pytest.approx([0.5 / hi, 0.5 / lo])
+    # the point estimate with frame's classified split of the ambiguous instructions (cndmask priced as such)
+    mix = {"sync": {"classes_per_item": {"fast": 60.0, "slow": 30.0, "trans": 10.0, "cnd": 2.0},
+                    "class_check_per_item": {k: {"model": v} for k, v in
+                                             (("fma_f32", 40.0), ("mul_f32", 5.0), ("add_f32", 5.0),
+                                              ("int64", 15.0), ("cvt", 5.0))}}}
+    split = mix_cap.frame_split(mix)
+    assert split == pytest.approx({"fast": 10 / 22, "slow": 10 / 22, "cnd": 2 / 22})
+    est = mix_cap.price_split(c, 3, split)
+    assert est == pytest.approx(200 / (k["fast"] * (50 + 30 * 10 / 22) + 10 * k["trans"] +
+                                       k["slow"] * (10 + 30 * 10 / 22) + k["cnd"] * 30 * 2 / 22))
+    assert est < hi
+    cap = b.issue_cap({"issue_model": {"method": "dynamic_split", "cap_frac": est, "cap_frac_range": [lo, hi],
+                                       "waves_per_simd": 3, "split_source": "x"}}, 0.5)
+    assert cap["issue_model_cap_frac"] == est and cap["frac_of_issue_model_cap"] == pytest.approx(0.5 / est)
 
 
 def test_classified_frame_cap(tmp_path):
