@@ -291,8 +291,8 @@ void fft64_quad_kernel(const float2 *__restrict__ in, float2 *__restrict__ out, 
 // VERDICT r4 item 6).  fft64_quad_kernel's lane q loads 16 B at byte 128 q + 16 c of its transform per
 // instruction, so one wave-instruction touches 64 different 128-B lines (and its stores 16 lines in 32-B pieces);
 // round 2's ablation priced perfectly coalesced loads at +9 % for fft (profiles/r02/k1q/fft_ab.txt).  Here a wave
-// owns 16 transforms (8 KB, contiguous in HBM):
-//   * loads: 8 LDS-DMA instructions (global_load_lds_dwordx4), each reading 1 KB of HBM contiguously; the lane ->
+// owns TPW = 8 transforms (4 KB, contiguous in HBM), quads 0..7 (lanes 0..31) transforming them:
+//   * loads: TPW / 2 LDS-DMA instructions (global_load_lds_dwordx4), each reading 1 KB of HBM contiguously; the lane ->
 //     chunk assignment inside each KB is permuted so that chunk j of transform t lands at slot 32 t + (j ^ s),
 //     s = 2 (t & 3) + (j >> 4): then the quad lanes' ds_read_b128 of "chunk 8 q + c" hit 16 distinct 4-bank groups
 //     in each of ds_read_b128's 16-lane groups ({0-3, 12-15, 20-27}, ...: transforms t, t + 3, t + 5, t + 6, whose
@@ -303,25 +303,34 @@ void fft64_quad_kernel(const float2 *__restrict__ in, float2 *__restrict__ out, 
 //     a 4 x 16 group write 16 distinct bank pairs), then each lane reads back 16 contiguous bytes (ds_read_b128,
 //     the XOR keeps a chunk's two bins adjacent) and writes them with one global_store_dwordx4: 1 KB contiguous per
 //     wave-instruction.
-// 32 KB of LDS per 256-thread block (5 blocks, 20 waves per CU).  In place (in == out) is safe: a wave reads all its
-// transforms before it writes them.
+// 16 KB of LDS per 256-thread block; 87 VGPRs hold it at 5 waves/SIMD.  In place (in == out) is safe: a wave reads all
+// its transforms before it writes them.
+// Transforms per wave (round 5, profiles/r05/ab/k1.txt): 16 (8 KB per wave, every lane busy) 5.39-5.48e9 transforms/s,
+// 8 (4 KB) 5.82-5.84e9 (+7 %), 4 (2 KB, 3/4 of the lanes idle) 4.17e9.  The same shapes as plain copies
+// (tools/ubench_copy.hip, profiles/r05/ab/copy_ceiling.txt): 8 KB per wave, loaded whole and then stored, 5.5-5.8 TB/s
+// whether staged through LDS or registers and at any occupancy; 4 KB 6.05; 2 KB 6.23; 1 KB 6.27-6.37 TB/s.
 #ifndef OFDM_K1_WPE
-#define OFDM_K1_WPE 4       // amdgpu_waves_per_eu lower bound: <= 128 VGPRs (95), so LDS (5 blocks per CU) sets occupancy
+#define OFDM_K1_WPE 4       // amdgpu_waves_per_eu lower bound: <= 128 VGPRs (87: 5 waves/SIMD; 6 spill 6 VGPRs)
 #endif
+#ifndef OFDM_K1_TPW
+#define OFDM_K1_TPW 8       // transforms per wave (16: every quad of the wave; 8 / 4: quads 0..TPW-1 only)
+#endif
+static_assert(OFDM_K1_TPW == 16 || OFDM_K1_TPW == 8 || OFDM_K1_TPW == 4, "whole 1-KB load / store instructions");
 #ifndef OFDM_K1_LOAD_CPOL
 #define OFDM_K1_LOAD_CPOL 2 // cache-policy bits of the LDS-DMA loads: nt (streamed once; A/B +1.5 % on top of the above)
 #endif
 template <bool INV, int CONV>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OFDM_K1_WPE)))
 void fft64_lds_kernel(const float2 *__restrict__ in, float2 *__restrict__ out, int64_t n) {
-    __shared__ __attribute__((aligned(16))) float4 buf[4][512];       // per wave: 16 transforms x 32 chunks of 16 B
+    constexpr int TPW = OFDM_K1_TPW;
+    __shared__ __attribute__((aligned(16))) float4 buf[4][32 * TPW];  // per wave: TPW transforms x 32 chunks of 16 B
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t t_base = ((int64_t)blockIdx.x * 4 + wv) * 16;       // this wave's first transform
+    const int64_t t_base = ((int64_t)blockIdx.x * 4 + wv) * TPW;      // this wave's first transform
     const int64_t avail = (n - t_base) * 32;                           // chunks of this wave that exist (>= 1)
     float4 *wb = buf[wv];
     const float4 *src = reinterpret_cast<const float4 *>(in) + t_base * 32;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < TPW / 2; ++i) {
         const int slot = 64 * i + lane, t = slot >> 5, jp = slot & 31;
         const int j = jp ^ (2 * (t & 3) + (jp >> 4));                  // the chunk whose slot this lane fills
         if (t * 32 + j < avail)
@@ -331,6 +340,8 @@ void fft64_lds_kernel(const float2 *__restrict__ in, float2 *__restrict__ out, i
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                  // this wave's DMA has landed (wave-private)
     const int q = lane & 3, tl = lane >> 2;                            // quad lane, transform within the wave
+    if (TPW < 16 && tl >= TPW) goto stores;                            // whole quads idle (TPW < 16)
+    {
     const int r = ((q & 1) << 1) | (q >> 1);                           // output residue of this lane
     const int64_t t = t_base + tl;
     const float s1 = q < 2 ? 1.0f : -1.0f;
@@ -386,6 +397,8 @@ void fft64_lds_kernel(const float2 *__restrict__ in, float2 *__restrict__ out, i
             ob[(4 * kp + r) ^ ox] = w;
         });
     }
+    }
+stores:
     // every lane's bins are in LDS before any lane reads its chunks back (one wave: LDS operations complete in
     // order; the fences keep the compiler from moving the reads above the writes)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -393,7 +406,7 @@ void fft64_lds_kernel(const float2 *__restrict__ in, float2 *__restrict__ out, i
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     float4 *dst = reinterpret_cast<float4 *>(out) + t_base * 32;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < TPW / 2; ++i) {
         const int g = 64 * i + lane, tg = g >> 5, m = g & 31;
         typedef const __attribute__((address_space(3))) f4v lf4c;
         const f4v v = *(lf4c *)(wb + 32 * tg + (m ^ (2 * (tg & 3))));
@@ -992,7 +1005,7 @@ __global__ __launch_bounds__(256, OFDM_RX_IDEAL_WAVES) void rx_ideal_kernel(RxAr
 template <bool INV>
 static void launch_fft_conv(int conv, dim3 g, hipStream_t st, const float2 *in, float2 *out, int64_t n) {
 #if OFDM_K1_LDS && !defined(OFDM_K1_LANE) && !defined(OFDM_K1_WAVE)
-    const dim3 gl((unsigned)((n + 63) / 64));
+    const dim3 gl((unsigned)((n + 4 * OFDM_K1_TPW - 1) / (4 * OFDM_K1_TPW)));
     if (conv == OFDM_CONV_C) hipLaunchKernelGGL((fft64_lds_kernel<INV, OFDM_CONV_C>), gl, dim3(256), 0, st, in, out, n);
     else hipLaunchKernelGGL((fft64_lds_kernel<INV, OFDM_CONV_MATLAB>), gl, dim3(256), 0, st, in, out, n);
     (void)g;
