@@ -44,7 +44,8 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BYTES_PER_SYMBOL_SNR = 652     # 80 x 8 B clean symbol + 12 B packed truth bits
 # wave64 VALU issue peak: 256 CUs x 4 SIMDs x 1 wave-instruction per 2 cycles at 2.4 GHz
 # (MI355X_MICROARCH.md "Wave scheduling"; tools/ubench_valu.hip)
-VALU_PEAK_PER_S = 256 * 4 * 0.5 * 2.4e9
+VALU_PEAK_GHZ = 2.4
+VALU_PEAK_PER_S = 256 * 4 * 0.5 * VALU_PEAK_GHZ * 1e9
 # capture samples read per trial (complex f32, from the L2-resident waveform): 3008 for the reference message,
 # int(0.307 x 19400) = 5955 for frame8's 8-symbol waveform (OFDM.c:945)
 FRAME_CAPTURE_SAMPLES = {"frame": 3008, "frame8": 5955}
@@ -160,6 +161,15 @@ def make_roofline(pmc: dict, lib_id: str | None, kernel: str, workload: str, uni
     frac = achieved / VALU_PEAK_PER_S
     model = pmc.get("issue_model")
     cap = issue_cap(pmc, frac) if model and model.get("build_id") == lib_id else {}
+    # the nominal peak assumes 2.4 GHz; the certified PMC run of the same command measured the SQ clock
+    # (GRBM_GUI_ACTIVE per XCD over the receiver dispatches): the same fractions at that clock separate the
+    # clock from the issue efficiency (this run's own clock is not measured)
+    clk = pmc.get("clock_ghz")
+    if clk and clk == clk:
+        scale = VALU_PEAK_GHZ / clk
+        cap = {**cap, "profiled_clock_ghz": clk, "frac_at_profiled_clock": frac * scale,
+               **({"frac_of_issue_model_cap_at_profiled_clock": cap["frac_of_issue_model_cap"] * scale}
+                  if "frac_of_issue_model_cap" in cap else {})}
     return {**base, "achieved": achieved, "frac": frac, "instr_per_unit": ipu,
             "pmc_source": "profiles/pmc_summary.json[%s]" % {"c4": "c3"}.get(workload, workload),
             **({"fused_tx": "the receivers build the step's Tx batches: chunk 0's its own (ofdm_txrx_frames), "

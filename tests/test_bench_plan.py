@@ -111,7 +111,13 @@ def test_roofline_needs_pmc_of_the_loaded_build(pkg):
     ok, traffic = b.make_roofline(_fake_pmc(lib_id), lib_id, *args)
     assert ok["frac"] == pytest.approx(4e7 * 52.6 / 3.4e-3 / b.VALU_PEAK_PER_S)
     assert ok["pmc_build_id"] == ok["lib_build_id"] == lib_id and traffic == 90.0 * 4e7
-    assert ok["issue_model_cap_frac"] == 0.585
+    assert ok["issue_model_cap_frac"] == 0.585 and "profiled_clock_ghz" not in ok
+    # with the SQ clock of the certified PMC run, the same fractions at that clock (clock vs issue efficiency)
+    clocked = {**_fake_pmc(lib_id), "clock_ghz": 2.2}
+    ck, _ = b.make_roofline(clocked, lib_id, *args)
+    assert ck["frac"] == ok["frac"] and ck["profiled_clock_ghz"] == 2.2
+    assert ck["frac_at_profiled_clock"] == pytest.approx(ok["frac"] * 2.4 / 2.2)
+    assert ck["frac_of_issue_model_cap_at_profiled_clock"] == pytest.approx(ok["frac"] / 0.585 * 2.4 / 2.2)
     mutated = lib_id[:-1] + ("0" if lib_id[-1] != "0" else "1")
     for pmc, why in ((_fake_pmc(mutated), "stale"), (_fake_pmc(None), "stale"), ({}, "no PMC"),
                      (_fake_pmc(lib_id, "rx_ls_kernel"), "launches")):
