@@ -339,6 +339,12 @@ __device__ __forceinline__ float2 cfo_rot(float2 v, double f_ts, int i) {
 //   * the sync wave that owns the item writes those whole lines (the round-3 [64 samples][ipb items][nw] tile
 //     wrote 32-B fragments 2 KB apart, 2.03x write amplification).
 constexpr int WIN_SG = 16;
+// frame_sym_kernel quads per item: 2 data lanes per quad for 1..2 data symbols (the reference frame: one quad),
+// 3 for longer messages (OFDM_FRAME_SYM_DPQ2=1: 2 always, the equivalence test)
+inline int sym_quads(int n_data) {
+    const int dpq = n_data <= 2 || getenv("OFDM_FRAME_SYM_DPQ2") ? 2 : 3;
+    return (n_data + dpq - 1) / dpq;
+}
 __host__ __device__ inline float2 *win_item(float2 *win, int ipb, int nw, int64_t item) {
     const int64_t tile = item / ipb, it = item - tile * ipb;
     return win + tile * 64 * (int64_t)(ipb * nw) + it * (WIN_SG * nw);
@@ -1195,8 +1201,11 @@ __global__ __launch_bounds__(64 * W, FRAME_SYNC_MINW) void frame_sync_kernel(Fra
 
 // ---------------------------------------------------------------- K4b': symbols of the synced frames
 // LS estimate + CP strip + fft + ZF + slicer + demap (OFDM.c:830-1165) for a batch of items: a quad
-// carries {LTF1, LTF2, D_2k, D_2k+1} of one item (estimate formed inside the quad with two DPP
-// broadcasts), ceil(n_data / 2) quads per item, 16 quads per wave.
+// carries the LTF-sum window in its lane 0 (the estimate, broadcast inside the quad by DPP) and dpq data
+// windows in its last dpq lanes: {LTF, LTF, D_2k, D_2k+1} for 1..2 data symbols and the reference frame's sweep,
+// {LTF, D_3k, D_3k+1, D_3k+2} for 3..8 (ceil(n_data / 3) quads per item instead of ceil(n_data / 2): the 8-symbol
+// message's items take 12 lanes, not 16).  The host picks dpq through the tile size a.ipb = 64 / quads per item
+// (sym_quads), from which the kernel derives it back.
 template <bool DUMP, int FIX_ND>   // DUMP: item 0's bits / subcarriers / metrics for ofdm_receiver
 #ifndef FRAME_SYM_MINB
 #define FRAME_SYM_MINB 2   // 3 waves/SIMD spills 196 VGPRs: frame mode 9 % slower
@@ -1205,22 +1214,27 @@ template <bool DUMP, int FIX_ND>   // DUMP: item 0's bits / subcarriers / metric
 __global__ __launch_bounds__(SYM_THREADS, FRAME_SYM_MINB) void frame_sym_kernel(FrameArgs a) {
     const int n_data = FIX_ND ? FIX_ND : a.n_data;
     __shared__ unsigned long long acc[OFDM_MAX_SNR][8];
-    __shared__ float part_e[SYM_THREADS / 4][2];             // per quad: EVM of its two data symbols
-    __shared__ uint32_t part_b[SYM_THREADS / 4][2], part_a[SYM_THREADS / 4][2];
+    constexpr int DPQ_MAX = FIX_ND ? 2 : 3;
+    __shared__ float part_e[SYM_THREADS / 4][DPQ_MAX];       // per quad: EVM of its data symbols
+    __shared__ uint32_t part_b[SYM_THREADS / 4][DPQ_MAX], part_a[SYM_THREADS / 4][DPQ_MAX];
     for (int k = threadIdx.x; k < a.n_snr * 8; k += SYM_THREADS) (&acc[0][0])[k] = 0ull;
     __syncthreads();
     const int lane = threadIdx.x & 63, quad = threadIdx.x >> 2, role = lane & 3;
-    const int qpi = (n_data + 1) / 2, ipb = (SYM_THREADS / 4) / qpi;   // quads per item, items per block
+    // quads per item and data lanes per quad: 2 with FIX_ND, else from the tile size (sym_quads)
+    const int qpi = FIX_ND ? (FIX_ND + 1) / 2 : (SYM_THREADS / 4) / a.ipb;
+    const int dpq = FIX_ND ? 2 : max(2, (n_data + qpi - 1) / qpi), r0 = 4 - dpq;   // first data role
+    const int ipb = (SYM_THREADS / 4) / qpi;                                // items per block
     const int item_l = quad / qpi, qi = quad - item_l * qpi;
-    const int dsym = 2 * qi + (role & 1);
+    const int dsym = dpq == 2 ? 2 * qi + (role & 1) : 3 * qi + max(role - 1, 0);
     const int nw = 1 + n_data;
     const int dsc = min(dsym, n_data - 1);
-    // role 0: the LTF-sum window (role 1 reads the same addresses and its transform is not used); 2, 3: data
-    const int w = role < 2 ? 0 : 1 + dsc;
+    // role 0: the LTF-sum window (with dpq = 2 role 1 reads the same addresses and its transform is not used);
+    // roles r0..3: data
+    const int w = role < r0 ? 0 : 1 + dsc;
     for (int64_t base = (int64_t)blockIdx.x * ipb; base < a.n_items; base += (int64_t)gridDim.x * ipb) {
         const int64_t i = base + item_l;
         const bool item_ok = item_l < ipb && i < a.n_items;
-        const bool dlane = item_ok && role >= 2 && dsym < n_data;
+        const bool dlane = item_ok && role >= r0 && dsym < n_data;
         const float2 *src = win_item(a.win, ipb, nw, item_ok ? i : base) + w;
         float2 x[64];
 #ifndef FRAME_SYM_GROUPS
@@ -1257,10 +1271,11 @@ __global__ __launch_bounds__(SYM_THREADS, FRAME_SYM_MINB) void frame_sym_kernel(
             demap_sub<DUMP, R, 2>(x, wd[R], Hof, deq, st);
             sched_fence();
         });
-        if (role >= 2) {
-            part_e[quad][role & 1] = dlane ? finish_evm<2>(st) : 0.f;
-            part_b[quad][role & 1] = dlane ? st.be : 0u;
-            part_a[quad][role & 1] = dlane ? st.ax : 0u;
+        if (role >= r0) {
+            const int sl = dpq == 2 ? role & 1 : role - 1;
+            part_e[quad][sl] = dlane ? finish_evm<2>(st) : 0.f;
+            part_b[quad][sl] = dlane ? st.be : 0u;
+            part_a[quad][sl] = dlane ? st.ax : 0u;
         }
         if (DUMP && dump && a.dbg_bits) { a.dbg_bits[3 * dsym] = st.d[0]; a.dbg_bits[3 * dsym + 1] = st.d[1]; a.dbg_bits[3 * dsym + 2] = st.d[2]; }
         __syncthreads();
@@ -1269,7 +1284,7 @@ __global__ __launch_bounds__(SYM_THREADS, FRAME_SYM_MINB) void frame_sym_kernel(
             float fe = 0.f;
             uint32_t ferr = 0u, fax = 0u;
             for (int k = 0; k < qpi; ++k)
-                for (int r2 = 0; r2 < 2; ++r2) {
+                for (int r2 = 0; r2 < dpq; ++r2) {
                     fe += part_e[quad + k][r2]; ferr += part_b[quad + k][r2]; fax += part_a[quad + k][r2];
                 }
             const int64_t g = a.item0 + i;
@@ -1327,7 +1342,7 @@ static unsigned occupancy_grid(const void *kernel, int threads, size_t lds, int 
 // K4b' (frame_sym_kernel) is instantiated in its own translation unit (ofdm_frame_sym.hip) so that the sync
 // kernel's can be compiled with another scheduler (build_lib.SOURCE_FLAGS); this is its launcher.
 void launch_frame_sym(hipStream_t st, const FrameArgs &a, int cus) {
-    const int ipb = (SYM_THREADS / 4) / ((a.n_data + 1) / 2);
+    const int ipb = a.ipb;
     const bool dump = a.dbg_eq || a.dbg_bits || a.dbg_res;
     const bool sym2 = a.n_data == 2 && !getenv("OFDM_FRAME_GENERIC");     // the hand-off offsets folded
     const void *k = dump ? reinterpret_cast<const void *>(&frame_sym_kernel<true, 0>)
@@ -1831,7 +1846,7 @@ static int run_frame_chunk(Ctx *c, FrameArgs &a) {
     a.trial0 = a.item0 / a.n_snr;
     a.q0 = (int32_t)(a.item0 % a.n_snr);
     a.snr_magic = 0xFFFFFFFFu / (uint32_t)a.n_snr;
-    a.ipb = (SYM_THREADS / 4) / ((a.n_data + 1) / 2);
+    a.ipb = (SYM_THREADS / 4) / sym_quads(a.n_data);
     const size_t wbytes = (size_t)((a.n_items + a.ipb - 1) / a.ipb) * a.ipb * nw * 64 * sizeof(float2);
     int rc = c->ensure(&c->d_scratch, &c->cap_scratch, wbytes + (size_t)a.n_items * sizeof(int4) + 256);
     if (rc) return rc;

@@ -202,6 +202,27 @@ def test_long_capture_kernel_equals_generic(pkg, monkeypatch, msg_len):
     assert lng[-1, 3] == 0                                           # 30 dB: error-free
 
 
+@pytest.mark.parametrize("msg_len", [96, 49, 30])
+def test_symbol_kernel_three_data_lanes_per_quad(pkg, monkeypatch, msg_len):
+    """Messages of 3..8 data symbols run frame_sym_kernel with quads {LTF, D, D, D} (ceil(n_data / 3) quads per
+    item; 12 lanes per 8-symbol item instead of 16).  Every counter and packet_idx equals the {LTF, LTF, D, D}
+    layout (OFDM_FRAME_SYM_DPQ2=1), for 8-, 5- and 3-symbol messages: the item totals are summed in symbol order
+    either way."""
+    snrs = np.array([0.0, 6.0, 10.0, 14.0, 20.0, 30.0])
+    msg = (b"three data lanes per quad in the symbol kernel, one lane for the LTF estimate. " * 2)[:msg_len]
+    with pkg.Engine(0) as e:
+        nd = e.set_message(msg)
+        assert nd == -(-8 * msg_len // 96) and nd >= 3
+        cfg = pkg.make_cfg(payload="message")
+        q3, p3 = e.frame_sweep(cfg, snrs, 2000, want_packet_idx=True, first_trial=5)
+        monkeypatch.setenv("OFDM_FRAME_SYM_DPQ2", "1")
+        q2, p2 = e.frame_sweep(cfg, snrs, 2000, want_packet_idx=True, first_trial=5)
+        monkeypatch.delenv("OFDM_FRAME_SYM_DPQ2")
+    assert np.array_equal(p3, p2)
+    assert np.array_equal(q3, q2)
+    assert q3[-1, 0] == 2000 and q3[-1, 3] == 0
+
+
 def test_frame_sweep_two_chunks_equal_their_halves(engine, pkg):
     """A sweep of more than 2^22 (trial, SNR) items runs as several sync -> symbol launch pairs through the
     hand-off buffer: its counters and packet_idx equal those of two sweeps of half the trials each (one
