@@ -1368,13 +1368,16 @@ void launch_frame_fix(hipStream_t st, const FrameArgs &a, dim3 grid, size_t lds)
 // Frames of 5..8 data symbols (ofdm_set_message) give captures of 4,482..5,955 samples: 18-24 KB of real parts per
 // wave, so frame_sync_kernel<0, 0> fits one four-wave block per CU (1 wave per SIMD).  This kernel keeps at most
 // LW_RES = 4,016 capture samples resident per wave (16 KB; two blocks, 2 waves per SIMD) by detecting in rounds
-// of 64 lanes x 31 positions (LW_ROUND = 1,984 positions, 2,031 samples each) and generating the capture in two
-// pieces, both from the same counter-based Philox stream as the whole capture:
-//   1. (three rounds only) samples [2 LW_ROUND, L) -> round 2 (positions [3,968, Lc));
-//   2. samples [0, min(L, LW_RES)) -> rounds 0 and 1 (the piece the matched filter almost always reads: the
-//      selected packet starts in the first frame period);
-//   3. when the matched filter's samples [p - 20, p + 2 (nfr - 1) + 10] leave the resident piece (the first
-//      valid front lies past ~2,070, ~9 % of 8-symbol trials), they are generated again into the region.
+// of 64 lanes x 31 positions (LW_ROUND = 1,984 positions, 2,031 samples each) and generating the capture in
+// pieces, all from the same counter-based Philox stream as the whole capture:
+//   1. samples [0, min(L, LW_RES)) -> rounds 0 and 1 (positions [0, 3,968): two frame periods);
+//   2. lazy (as frame_sync_kernel's, one round later): Packet_Selection is decided by rounds 0 and 1 when their
+//      least valid front (its +230 check inside them) has a later front inside them: fronts and checks depend
+//      only on earlier positions, and every later front lies past it.  Then round 2 and its samples are skipped;
+//   3. otherwise samples [2 LW_ROUND, L) over the region -> round 2 (positions [3,968, Lc)) and the selection
+//      over all three rounds (a.no_lazy: always);
+//   4. when the matched filter's samples [p - 20, p + 2 (nfr - 1) + 10] are not resident (the first valid front
+//      past ~2,070, or piece 1 overwritten by step 3), they are generated again into the region.
 // The filtered frame fr[] then overwrites the region: a lane holds its runs' outputs in registers until every
 // lane's reads are done.  Packet detection / selection, the matched filter, CFO and hand-off are the generic
 // kernel's arithmetic, so every counter and packet_idx equals frame_sync_kernel<0, 0>'s
@@ -1501,15 +1504,7 @@ __global__ __launch_bounds__(64 * W, FRAME_LONG_MINW) void frame_sync_long_kerne
             first[rho] = cmask ? n0 + __builtin_ctzll(cmask) : -1;
             last[rho] = cmask ? n0 + 63 - __builtin_clzll(cmask) : -1;
         };
-        // piece 1 (three rounds): samples [2 LW_ROUND, L) at region float off + n - LW_ROUND, round 2
-        if (R == 3) {
-            capture_blocks(a, wave_len, rbase, b0 + LW_ROUND / 4, (rx_start + 2 * LW_ROUND) >> 2, (rx_start + L - 1) >> 2,
-                           lane, t_lo, t_hi, qs, sigma);
-            wave_lds_sync();
-            detect(std::integral_constant<int, 2>{}, r - LW_ROUND);
-            wave_lds_sync();                                  // every lane's loads are done: piece 2 overwrites
-        }
-        // piece 2: samples [0, min(L, LW_RES)), rounds 0 and 1
+        // piece 1: samples [0, min(L, LW_RES)), rounds 0 and 1
         const int res_end = min(L, LW_RES);
         capture_blocks(a, wave_len, rbase, b0, b0, (rx_start + res_end - 1) >> 2, lane, t_lo, t_hi, qs, sigma);
         wave_lds_sync();
@@ -1530,30 +1525,48 @@ __global__ __launch_bounds__(64 * W, FRAME_LONG_MINW) void frame_sync_long_kerne
             });
             return ((w >> bit) & 1ull) != 0ull;
         };
-        // ---- Packet_Selection (OFDM.c:685-771) over the R rounds (frame_sync_kernel's rule) ----
-        int vmin = 0x7fffffff, fmax_ = -1, carry = -1;
-        static_for<0, 3>([&](auto rc) {
-            constexpr int rho = decltype(rc)::value;
-            if (rho < R) {
-                const int pm = max(wave_prefix_max(last[rho]), carry);
-                const int prev = max(wave_shr1(pm), carry);
-                const int front = (first[rho] >= 0 && first[rho] - prev > 300) ? first[rho] : -1;
-                carry = __builtin_amdgcn_readlane(pm, 63);
-                const int pos = front + 230;
-                const bool valid = crossing(pos < Lc ? pos : 0) && front >= 0 && pos < Lc;
-                vmin = min(vmin, valid ? front : 0x7fffffff);
-                fmax_ = max(fmax_, front);
+        // ---- Packet_Selection (OFDM.c:685-771) over the first nr rounds (frame_sync_kernel's rule); a front whose
+        // +230 check lies at or past `limit` is not valid (not known yet) ----
+        auto select = [&](int nr, int limit) {
+            int vmin = 0x7fffffff, fmax_ = -1, carry = -1;
+            static_for<0, 3>([&](auto rc) {
+                constexpr int rho = decltype(rc)::value;
+                if (rho < nr) {
+                    const int pm = max(wave_prefix_max(last[rho]), carry);
+                    const int prev = max(wave_shr1(pm), carry);
+                    const int front = (first[rho] >= 0 && first[rho] - prev > 300) ? first[rho] : -1;
+                    carry = __builtin_amdgcn_readlane(pm, 63);
+                    const int pos = front + 230;
+                    const bool valid = crossing(pos < limit ? pos : 0) && front >= 0 && pos < limit;
+                    vmin = min(vmin, valid ? front : 0x7fffffff);
+                    fmax_ = max(fmax_, front);
+                }
+            });
+            const int cmin = wave_min_i(vmin), cmax = wave_max_i(fmax_);
+            return cmin < cmax ? cmin : 0x7fffffff;
+        };
+        // lazy: rounds 0 and 1 decide when their least valid front has a later front in them (the full rule then
+        // picks the same front: see the header); otherwise round 2 over the region and the selection over all rounds
+        int cand = R == 3 && !a.no_lazy ? select(2, min(2 * LW_ROUND, Lc)) : 0x7fffffff;
+        bool res1 = true;                                     // piece 1 still in the region
+        if (cand == 0x7fffffff) {
+            if (R == 3) {
+                wave_lds_sync();                              // rounds 0-1's loads are done: piece 2 overwrites
+                capture_blocks(a, wave_len, rbase, b0 + LW_ROUND / 4, (rx_start + 2 * LW_ROUND) >> 2,
+                               (rx_start + L - 1) >> 2, lane, t_lo, t_hi, qs, sigma);
+                wave_lds_sync();
+                detect(std::integral_constant<int, 2>{}, r - LW_ROUND);   // sample n at region float off + n - LW_ROUND
+                res1 = false;
             }
-        });
-        const int cmin = wave_min_i(vmin), cmax = wave_max_i(fmax_);
-        const int cand = cmin < cmax ? cmin : 0x7fffffff;
+            cand = select(R, Lc);
+        }
         const bool sync_fail = cand == 0x7fffffff;
         const int p = sync_fail ? 0 : cand + 10 + 1;
         // ---- the matched filter's samples [p - 20, p + 2 (nfr - 1) + 10]: resident, or generated again ----
         const float *rm = r;
         {
             const int lo = max(p - 20, 0), hi = min(p + 2 * (nfr - 1) + 10, L - 1);
-            if (hi >= res_end) {
+            if (hi >= res_end || !res1) {
                 const int s0 = lo & ~3;
                 wave_lds_sync();                              // detection's loads are done
                 capture_blocks(a, wave_len, rbase, (rx_start + s0) >> 2, (rx_start + s0) >> 2, (rx_start + hi) >> 2, lane,

@@ -202,6 +202,25 @@ def test_long_capture_kernel_equals_generic(pkg, monkeypatch, msg_len):
     assert lng[-1, 3] == 0                                           # 30 dB: error-free
 
 
+def test_long_capture_lazy_equals_full_evaluation(pkg, monkeypatch):
+    """frame_sync_long_kernel skips detection round 2 and its capture samples when rounds 0 and 1 decide
+    Packet_Selection (their least valid front has a later front in them).  Every counter and packet_idx equals the
+    evaluation of every round (OFDM_FRAME_NO_LAZY=1), over the bench's SNR grid, where low-SNR items need round 2
+    (noise fronts) and high-SNR ones do not."""
+    snrs = np.arange(0.0, 31.0, 2.0)
+    msg = (b"lazy rounds for the long-capture kernel: two frame periods decide most trials. " * 2)[:96]
+    with pkg.Engine(0) as e:
+        assert e.set_message(msg) == 8
+        cfg = pkg.make_cfg(payload="message")
+        lz, lp = e.frame_sweep(cfg, snrs, 1500, want_packet_idx=True, first_trial=7)
+        monkeypatch.setenv("OFDM_FRAME_NO_LAZY", "1")
+        fu, fp = e.frame_sweep(cfg, snrs, 1500, want_packet_idx=True, first_trial=7)
+        monkeypatch.delenv("OFDM_FRAME_NO_LAZY")
+    assert np.array_equal(lp, fp)
+    assert np.array_equal(lz, fu)
+    assert np.mean(lp[-4:] > 0) > 0.99
+
+
 @pytest.mark.parametrize("msg_len", [96, 49, 30])
 def test_symbol_kernel_three_data_lanes_per_quad(pkg, monkeypatch, msg_len):
     """Messages of 3..8 data symbols run frame_sym_kernel with quads {LTF, D, D, D} (ceil(n_data / 3) quads per

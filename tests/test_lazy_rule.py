@@ -1,8 +1,9 @@
-"""The frame sync kernel's lazy capture rule (ofdm_frame.hip, FRAME_LAZY) against the
-reference's own Packet_Selection (src/OFDM.c:685-771, compiled in oracle/_ref) on random captures of the
-reference waveform: whenever the first detection round [0, 64 x 31) decides the selection by the kernel's
-rule, the reference's packet_idx over the WHOLE capture is that decision.  (The GPU test
-test_lazy_capture_equals_full_evaluation checks the kernel's lazy and full paths against each other.)"""
+"""The frame sync kernels' lazy rules (ofdm_frame.hip: FRAME_LAZY, and frame_sync_long_kernel's round-2 skip;
+DESIGN.md §4 K4b) against the reference's own Packet_Selection (src/OFDM.c:685-771, compiled in oracle/_ref) on
+random captures: whenever the first detection round [0, 64 x 31) (reference message) or the first two rounds
+[0, 2 x 64 x 31) (8-symbol message) decide the selection by the kernel's rule, the reference's packet_idx over
+the WHOLE capture is that decision.  (The GPU tests test_lazy_capture_equals_full_evaluation and
+test_long_capture_lazy_equals_full_evaluation check the kernels' lazy and full paths against each other.)"""
 import ctypes as C
 
 import numpy as np
@@ -57,3 +58,39 @@ def test_round0_decision_is_the_references(reflib, snr_db):
             assert ref == p, (snr_db, s)
     if snr_db >= 12:
         assert decided > 0.6 * 400                                  # the rule does skip work where sync works
+
+
+def rounds_decision(m, limit):
+    """frame_sync_long_kernel's rule: (decided, packet_idx) from the positions below `limit` alone"""
+    idx = np.nonzero(m[:limit] > 0.75)[0]
+    if len(idx) == 0:
+        return False, None
+    prev = np.concatenate([[-1], idx[:-1]])
+    fronts = idx[(idx - prev) > 300]
+    valid = [f for f in fronts if f + 230 < limit and m[f + 230] > 0.75]
+    if not valid or valid[0] >= fronts.max():
+        return False, None
+    return True, int(valid[0]) + LEN_RRC_RX + 1
+
+
+@pytest.mark.parametrize("snr_db", [0.0, 6.0, 10.0, 16.0, 30.0])
+def test_long_frames_two_round_decision_is_the_references(oracle, reflib, snr_db):
+    msg = (b"lazy rounds for the long-capture kernel: two frame periods decide most trials. " * 2)[:96]
+    assert oracle.set_message(msg) == 8
+    wave = oracle.frame_waveform(oracle.message_bits(msg)).astype(np.complex128)
+    L = int(0.307 * len(wave))
+    assert L == 5955
+    rng = np.random.default_rng(int(snr_db * 10) + 3)
+    sigma = np.sqrt(np.mean(np.abs(wave) ** 2) / 10 ** (snr_db / 10))
+    decided = 0
+    for _ in range(150):
+        s = int(rng.integers(0, len(wave) - L))
+        cap = wave[s:s + L] + sigma * rng.standard_normal(L)        # real-only AWGN (D7)
+        m = corr_out(cap)
+        ok, p = rounds_decision(m, 2 * B1)
+        if ok:
+            decided += 1
+            ref = reflib.lib.ref_packet_selection(m.ctypes.data_as(C.c_void_p), len(m))
+            assert ref == p, (snr_db, s)
+    if snr_db >= 16:
+        assert decided > 0.8 * 150                                  # round 2 is skipped where sync works
