@@ -76,8 +76,7 @@ def rounds_decision(m, limit):
 @pytest.mark.parametrize("snr_db", [0.0, 6.0, 10.0, 16.0, 30.0])
 def test_long_frames_two_round_decision_is_the_references(oracle, reflib, snr_db):
     msg = (b"lazy rounds for the long-capture kernel: two frame periods decide most trials. " * 2)[:96]
-    assert oracle.set_message(msg) == 8
-    wave = oracle.frame_waveform(oracle.message_bits(msg)).astype(np.complex128)
+    wave = oracle.frame_waveform(oracle.message_bits(msg)).astype(np.complex128)     # the oracle's message is untouched
     L = int(0.307 * len(wave))
     assert L == 5955
     rng = np.random.default_rng(int(snr_db * 10) + 3)
