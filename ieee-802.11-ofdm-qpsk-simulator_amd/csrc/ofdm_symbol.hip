@@ -340,8 +340,7 @@ void fft64_lds_kernel(const float2 *__restrict__ in, float2 *__restrict__ out, i
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                  // this wave's DMA has landed (wave-private)
     const int q = lane & 3, tl = lane >> 2;                            // quad lane, transform within the wave
-    if (TPW < 16 && tl >= TPW) goto stores;                            // whole quads idle (TPW < 16)
-    {
+    if (TPW == 16 || tl < TPW) {                                       // whole quads idle past TPW
     const int r = ((q & 1) << 1) | (q >> 1);                           // output residue of this lane
     const int64_t t = t_base + tl;
     const float s1 = q < 2 ? 1.0f : -1.0f;
@@ -398,7 +397,6 @@ void fft64_lds_kernel(const float2 *__restrict__ in, float2 *__restrict__ out, i
         });
     }
     }
-stores:
     // every lane's bins are in LDS before any lane reads its chunks back (one wave: LDS operations complete in
     // order; the fences keep the compiler from moving the reads above the writes)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
