@@ -21,8 +21,11 @@ Workloads (BASELINE.json configs; --workload):
                            a step = one fft + one ifft over the HBM-resident batch; HBM roofline at 1,024 B per
                            transform (512 B read + 512 B written); units are transforms (one OFDM symbol each)
 
-Launched as `python bench.py --gpus N --steps K --warmup W`, or for N > 1 under
-`torch.distributed.run` (one rank per GPU, RCCL all-reduce).  Rank 0 prints ONE JSON line.
+Launched as `python bench.py --gpus N --steps K --warmup W`.  For N > 1 outside torchrun, bench.py starts
+`torch.distributed.run --nproc-per-node N` on itself as a child process (launch_ranks; it never execs) and
+relays rank 0's line; under torchrun every rank checks WORLD_SIZE == --gpus.  One rank per GPU, RCCL all-reduce
+of the counters; OFDM_DIST_BACKEND=gloo reduces host copies instead (several ranks sharing one GPU: the tests'
+world-2 run on a 1-GPU box).  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -77,6 +80,7 @@ WORKLOADS = {
     "fft64": ("K1: batched 64-point fft() + ifft() (C convention) of HBM-resident symbols, 2^24 transforms per "
               "launch", {}, 1 << 24, "weak"),
 }
+COLLECTIVE = {"nccl": "RCCL", "gloo": "gloo (host copy)"}
 FFT_BYTES_PER_TRANSFORM = 1024     # 64 complex f32 read + 64 written
 STEP_DEFAULTS = {"c2": (50, 10)}   # (steps, warmup) when not given
 # data symbols per frame (trial) of each workload; frame8 sets its message before the sweep
@@ -416,7 +420,7 @@ class PipelinedSymbolStep:
             rx_done[k].record(s_rx)
 
 
-def run_fft64(args, cpu, torch, dist, pkg, abi, codeobj, rank, world, dev, distributed):
+def run_fft64(args, cpu, torch, dist, pkg, abi, codeobj, rank, world, dev, distributed, backend):
     """--workload fft64: K1 (ofdm_fft64) alone on an HBM-resident batch of 2^24 symbols per GPU (weak scaling).  A
     step is fft() of the batch into a second buffer and ifft() back (C convention, OFDM.c:314-339): two launches,
     2^25 transforms.  The roofline is HBM: 1,024 algorithmic bytes per transform over the launches' HIP-event time
@@ -435,7 +439,7 @@ def run_fft64(args, cpu, torch, dist, pkg, abi, codeobj, rank, world, dev, distr
         eng.fft64_into(x, y, inverse=False)
         eng.fft64_into(y, x, inverse=True)
         if distributed:
-            dist.all_reduce(done, op=dist.ReduceOp.SUM)      # the job's one collective (a completion count)
+            host_allreduce(dist, done, dist.ReduceOp.SUM)    # the job's one collective (a completion count)
 
     x0 = x[:4].clone()
     for _ in range(args.warmup):
@@ -457,8 +461,7 @@ def run_fft64(args, cpu, torch, dist, pkg, abi, codeobj, rank, world, dev, distr
     ms, launches = eng.timing_query(abi.K_FFT)
     if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+        elapsed = host_allreduce(dist, t, dist.ReduceOp.MAX).item()
     # ifft(fft(x)) in the reference's C convention is x circularly shifted by 32 samples (fftshift of the IDFT,
     # SURVEY D5): after an odd number of steps the first vectors are x0 rolled by 32, after an even number x0 (a
     # cheap check that the launches did the work)
@@ -480,8 +483,10 @@ def run_fft64(args, cpu, torch, dist, pkg, abi, codeobj, rank, world, dev, distr
             "vs_baseline": None, "dtype": "f32", "data": "synthetic (torch.randn complex64, seed 0x80211A + rank)",
             "config": {"workload": "fft64", "description": desc, "transforms_per_launch_per_gpu": n,
                        "launches_per_step": 2, "conv": "c",
-                       "parallelism": (f"dp{world} (each rank its own batch, weak scaling)" if distributed
-                                       else "1 process, no collective (not launched under torchrun)")},
+                       "parallelism": (f"dp{world} (each rank its own batch, weak scaling; 1 {COLLECTIVE[backend]} "
+                                       "all-reduce of a completion count per step)" if distributed
+                                       else "1 process, no collective (not launched under torchrun)"),
+                       "backend": backend if distributed else None},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": tpu * units_per_launch if tpu else None,
@@ -501,8 +506,71 @@ def run_fft64(args, cpu, torch, dist, pkg, abi, codeobj, rank, world, dev, distr
 
 
 def wants_cpu_baseline(args) -> bool:
-    """Rank 0 of the job times the reference (any WORLD_SIZE); the others do not."""
+    """Rank 0 of the job times the reference (any WORLD_SIZE); the others do not.  A self-launching parent
+    (launch_ranks) never does: its rank 0 child does."""
     return int(os.environ.get("RANK", "0")) == 0 and not args.no_cpu_baseline
+
+
+def _free_port() -> int:
+    import socket  # noqa: PLC0415
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def child_command(n: int, argv: list[str], port: int) -> list[str]:
+    """The torchrun command line of `bench.py --gpus n` started outside torchrun: one rank per GPU of this node,
+    rendezvous on 127.0.0.1, the same bench arguments (each rank then sees WORLD_SIZE == --gpus)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", str(ROOT / "bench.py"), *argv]
+
+
+def launch_ranks(n: int, argv: list[str]) -> int:
+    """`--gpus n > 1` outside torchrun: start the n ranks under torch.distributed.run as a CHILD process (this
+    process never touches the GPU and never execs), pass its output through and relay rank 0's JSON line as the
+    one line on stdout.  Returns the child's exit status (non-zero also when no JSON line came back)."""
+    import subprocess  # noqa: PLC0415
+    cmd = child_command(n, argv, _free_port())
+    print("bench.py: launching %d ranks: %s" % (n, " ".join(cmd)), file=sys.stderr, flush=True)
+    env = dict(os.environ, PYTHONUNBUFFERED="1")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env, cwd=str(ROOT))
+    lines = []
+    for ln in proc.stdout:                 # streamed: progress reaches the log while the ranks run
+        s = ln.strip()
+        if s.startswith("{") and '"metric"' in s:
+            lines.append(s)
+        else:
+            sys.stderr.write(ln)
+            sys.stderr.flush()
+    rc = proc.wait()
+    if rc != 0:
+        print(f"bench.py: the {n}-rank child exited with {rc}", file=sys.stderr)
+        return rc
+    if len(lines) != 1:
+        print(f"bench.py: expected one JSON line from rank 0, got {len(lines)}", file=sys.stderr)
+        return 1
+    print(lines[0], flush=True)
+    return 0
+
+
+def check_world(args) -> None:
+    """Under torchrun every rank must see WORLD_SIZE == --gpus: a line's n_gpus is the world size, so a mismatch
+    would report a different job than the one asked for."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
+
+
+def host_allreduce(dist, t, op):
+    """all_reduce of a device tensor through a host copy (gloo: several ranks sharing one GPU, or CPU tests);
+    RCCL reduces it in HBM"""
+    if dist.get_backend() == "nccl":
+        dist.all_reduce(t, op=op)
+        return t
+    h = t.cpu()
+    dist.all_reduce(h, op=op)
+    t.copy_(h)
+    return t
 
 
 def main():
@@ -524,6 +592,12 @@ def main():
     dflt = STEP_DEFAULTS.get(args.workload, (5, 2))
     args.steps = dflt[0] if args.steps is None else args.steps
     args.warmup = dflt[1] if args.warmup is None else args.warmup
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if "RANK" not in os.environ and args.gpus > 1:
+        # one rank per GPU: this process only launches them (nothing here touches the GPU)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    check_world(args)
 
     # host-side reference timing first, before anything touches the GPU (worker processes are spawned).
     # Under torchrun rank 0 (local rank 0 of the one node) times it before forming the process group; the
@@ -536,15 +610,18 @@ def main():
     from ofdm_amd import abi, codeobj, dist as odist
 
     rank, world, local = odist.env_rank_world()
-    # under torch.distributed.run (RANK set) the RCCL group is formed even for one rank, and the
-    # counters' all-reduce runs through it
+    # under torch.distributed.run (RANK set) the group is formed even for one rank, and the counters' all-reduce
+    # runs through it: RCCL (one rank per GPU), or gloo with OFDM_DIST_BACKEND=gloo (ranks may share a GPU)
     distributed = "RANK" in os.environ
+    backend = os.environ.get("OFDM_DIST_BACKEND", "nccl")
+    dev = 0
     if distributed:
-        odist.init_from_env("nccl")
-    dev = local if distributed else 0
+        dev = local if backend == "nccl" else local % max(torch.cuda.device_count(), 1)
+        odist.init_from_env(backend, device=dev)
+        torch.cuda.set_device(dev)
 
     if args.workload == "fft64":
-        run_fft64(args, cpu, torch, dist, pkg, abi, codeobj, rank, world, dev, distributed)
+        run_fft64(args, cpu, torch, dist, pkg, abi, codeobj, rank, world, dev, distributed, backend)
         return
     desc, kw, symbols, scaling = WORKLOADS[args.workload]
     if args.symbols:
@@ -581,7 +658,7 @@ def main():
         else:
             counters.zero_()      # a rank without frames (strong split of a tiny job)
         if distributed:
-            dist.all_reduce(counters, op=dist.ReduceOp.SUM)     # RCCL over xGMI (a copy at world 1)
+            host_allreduce(dist, counters, dist.ReduceOp.SUM)   # RCCL over xGMI (a copy at world 1)
 
     for _ in range(args.warmup):
         step()
@@ -603,8 +680,7 @@ def main():
     tx_ms, tx_n = eng.timing_query(abi.K_TX)
     if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+        elapsed = host_allreduce(dist, t, dist.ReduceOp.MAX).item()
 
     c = counters.cpu().numpy()
     n_snr = len(SNR_GRID)
@@ -645,9 +721,10 @@ def main():
                        "symbols_per_snr": symbols if scaling == "strong" else symbols * world,
                        "symbols_per_snr_per_gpu": dpf * frames, "snr_db": SNR_GRID.tolist(),
                        "frames_per_gpu": frames, "data_symbols_per_frame": dpf, "chunks_per_step": len(chunks),
-                       "parallelism": (f"dp{world} (counter-range shards, {scaling} scaling; 1 RCCL all-reduce of "
-                                       "int64 counters per step)" if distributed
-                                       else "1 process, no collective (not launched under torchrun)")},
+                       "parallelism": (f"dp{world} (counter-range shards, {scaling} scaling; 1 {COLLECTIVE[backend]} "
+                                       "all-reduce of int64 counters per step)" if distributed
+                                       else "1 process, no collective (not launched under torchrun)"),
+                       "backend": backend if distributed else None},
             # the binding roofline: VALU issue (make_roofline)
             "roofline": roofline,
             # HBM: the measured traffic (PMC) against the HBM peak is the HBM roofline fraction.  SURVEY

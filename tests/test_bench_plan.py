@@ -468,3 +468,46 @@ def test_c2_breakdown(tmp_path):
     st.write_text("pack stamp wave 0: item-top barrier 5.00%; prologue work 20.00%; SNR loop 75.00%;\n"
                   "pack stamp wave 2: item-top barrier 1.00%; prologue work 9.00%; SNR loop 90.00%;\n")
     assert c2_breakdown.stamps(st) == {"item-top barrier": 0.05, "prologue work": 0.2, "SNR loop": 0.75}
+
+
+def test_child_command_runs_n_ranks_of_the_same_bench():
+    """`bench.py --gpus N` outside torchrun starts N ranks under torch.distributed.run as a child
+    (127.0.0.1 rendezvous), with the same bench arguments, so every rank sees WORLD_SIZE == --gpus."""
+    b = _bench()
+    argv = ["--gpus", "4", "--workload", "c4", "--steps", "3"]
+    cmd = b.child_command(4, argv, 29555)
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "--nnodes=1" in cmd and "--master-addr=127.0.0.1" in cmd
+    assert "--master-port=29555" in cmd
+    i = cmd.index(str(ROOT / "bench.py"))
+    assert cmd[i + 1:] == argv
+
+
+@pytest.mark.parametrize("world,gpus", [("3", "2"), ("1", "8"), ("2", "1")])
+def test_world_size_must_equal_gpus(world, gpus):
+    """Under torchrun a rank whose WORLD_SIZE differs from --gpus exits non-zero before anything is timed or
+    touches the GPU (no line can carry n_gpus != --gpus)."""
+    import os
+    import subprocess
+    env = dict(os.environ, RANK="0", LOCAL_RANK="0", WORLD_SIZE=world)
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", gpus, "--no-cpu-baseline"],
+                       capture_output=True, text=True, timeout=120, env=env, cwd=str(ROOT))
+    assert r.returncode != 0 and f"WORLD_SIZE={world} but --gpus {gpus}" in r.stderr
+    assert r.stdout.strip() == ""
+
+
+def test_launch_ranks_relays_one_line(monkeypatch, capsys):
+    """launch_ranks passes the child's other output to stderr, relays exactly one JSON line on stdout, and
+    returns non-zero when the child fails or no line (or more than one) comes back."""
+    b = _bench()
+    line = json.dumps({"metric": "m", "value": 1.0, "n_gpus": 2})
+    for script, rc_want, out_want in ((f"print('progress'); print({line!r})", 0, line),
+                                      (f"print({line!r}); raise SystemExit(3)", 3, ""),
+                                      ("print('no line')", 1, ""),
+                                      (f"print({line!r}); print({line!r})", 1, "")):
+        monkeypatch.setattr(b, "child_command", lambda n, argv, port, _s=script: [sys.executable, "-c", _s])
+        rc = b.launch_ranks(2, [])
+        out = capsys.readouterr()
+        assert rc == rc_want and out.out.strip() == out_want, script
+        if rc_want == 0:
+            assert "progress" in out.err

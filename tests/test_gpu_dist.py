@@ -152,3 +152,35 @@ def test_torchrun_bench_rccl(workload, symbols):
     assert "RCCL all-reduce" in line["config"]["parallelism"]
     assert line["results"]["frames_per_snr"] == symbols // 2
     assert line["scaling"] == ("weak" if workload == "c3" else "strong")
+
+
+@pytest.mark.parametrize("workload,symbols,frames_per_snr",
+                         [("c3", 200_000, 2 * 100_000),     # weak: each rank its own 100,000 frames
+                          ("c4", 400_000, 200_000),         # strong: 200,000 frames in total, split over 2 ranks
+                          ("fft64", 1 << 16, None)])
+def test_bench_gpus2_self_launch_gloo(workload, symbols, frames_per_snr):
+    """`bench.py --gpus 2` outside torchrun launches its own 2 ranks (torch.distributed.run as a
+    child) and relays rank 0's line.  On this 1-GPU box the ranks share cuda:0 and reduce over gloo
+    (OFDM_DIST_BACKEND=gloo; RCCL refuses two ranks on one GPU): the weak/strong range split, the per-step
+    counter all-reduce, the max-over-ranks time and the whole-job value run at world 2 (the sharded trial loop,
+    /root/reference/src/OFDM.c:1195-1222)."""
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--workload", workload, "--symbols", str(symbols),
+           "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+    env = dict(os.environ, PYTHONUNBUFFERED="1", OFDM_DIST_BACKEND="gloo")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=str(ROOT))
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = r.stdout.strip().splitlines()
+    assert len(out) == 1, out
+    line = json.loads(out[0])
+    assert line["n_gpus"] == 2 and line["value"] > 0
+    assert line["config"]["parallelism"].startswith("dp2") and line["config"]["backend"] == "gloo"
+    if frames_per_snr is None:
+        # weak: both ranks' 2 launches x 2^16 transforms per step
+        assert line["value"] == pytest.approx(2 * 2 * symbols * line["steps"] / (line["ms_per_step"] * line["steps"] / 1e3))
+        assert line["results"]["fft_ifft_roundtrip_max_rel_err"] < 1e-5
+        return
+    assert line["results"]["frames_per_snr"] == frames_per_snr
+    per_gpu = symbols // 2 if workload == "c3" else symbols // 2 // 2
+    assert line["config"]["frames_per_gpu"] == per_gpu
+    units = frames_per_snr * 2 * 16 * line["steps"]
+    assert line["value"] == pytest.approx(units / (line["ms_per_step"] * line["steps"] / 1e3))
