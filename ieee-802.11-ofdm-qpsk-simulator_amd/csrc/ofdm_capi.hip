@@ -462,10 +462,6 @@ static int rx_common(Ctx *c, const ofdm_cfg *cfg, const void *d_tx, const void *
             const double s2 = cfg->kappa * cfg->p_ref / std::pow(10.0, snr_db[q0 + q] / 10.0);
             a.sigma[q] = (float)std::sqrt(s2);
         }
-#ifdef OFDM_RX_STAMPS
-        HIPOK(hipMalloc(&a.stamps, 64));
-        HIPOK(hipMemset(a.stamps, 0, 64));
-#endif
         if (fuse_nx && q0 == 0) {
             a.nx = tx_args(c, &c->nx_cfg, c->nx_first, c->nx_n, c->nx_tx, c->nx_bits);
             a.nx_conv = c->nx_cfg.conv;
@@ -481,18 +477,6 @@ static int rx_common(Ctx *c, const ofdm_cfg *cfg, const void *d_tx, const void *
         launch_rx(c->stream, a, *cfg, dump, grid);
         c->toc();
         HIPOK(hipGetLastError());
-#ifdef OFDM_RX_STAMPS
-        unsigned long long hs[5];
-        HIPOK(hipMemcpy(hs, a.stamps, sizeof(hs), hipMemcpyDeviceToHost));
-        hipFree(a.stamps);
-        static const char *names[5] = {"window+noise+stage1", "sub-block FFTs", "eq fetch + demap",
-                                       "metrics + counters", "group end"};
-        double tot = 0;
-        for (double v : hs) tot += v;
-        for (int k = 0; k < 5; ++k)
-            fprintf(stderr, "rx stamp %-20s %6.2f%%  %.1f wave-cycles per symbol-SNR\n", names[k],
-                    100.0 * hs[k] / tot, (double)hs[k] / (2.0 * n_frames * a.n_snr));
-#endif
     }
     return OFDM_OK;
 }

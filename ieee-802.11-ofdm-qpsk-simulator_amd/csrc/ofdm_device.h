@@ -183,17 +183,8 @@ __device__ __forceinline__ void philox10_c2_vk(const PhiloxHead &h, const uint32
 }
 
 // The Box-Muller angle of a Philox word x, in revolutions (v_sin / v_cos take revolutions).
-// OFDM_BM_ANGLE_BITS (A/B option): 1 + (x >> 9) 2^-23 in [1, 2) built by one v_alignbit (the exponent bits
-// shifted in from a constant) instead of v_cvt_f32_u32 + v_mul.
-#ifndef OFDM_BM_ANGLE_BITS
-#define OFDM_BM_ANGLE_BITS 0
-#endif
 __device__ __forceinline__ float bm_angle(uint32_t x) {
-#if OFDM_BM_ANGLE_BITS
-    return __uint_as_float(__builtin_amdgcn_alignbit(0x7Fu, x, 9));
-#else
     return (float)x * 0x1p-32f;
-#endif
 }
 
 // Box-Muller pair.  u1 = fma((float)x1, 2^-32, 2^-33) in (0, 1] (tail to 6.7 sigma);
@@ -309,11 +300,7 @@ __device__ __forceinline__ int lane_fresh() {
     return l;
 }
 
-#ifndef OFDM_NO_SCHED_FENCE
 __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
-#else
-__device__ __forceinline__ void sched_fence() {}
-#endif
 
 // global-address-space views (keep loads global_* after opaque(), which erases provenance).
 // Native clang vectors, not float2 (HIP_vector_type's members are not address-space qualified).

@@ -371,9 +371,7 @@ __device__ __forceinline__ int needed_k(int j) {
 // a capture's imaginary part IS the clean waveform's, so each wave stores only the real parts of its
 // capture) and the per-SNR accumulators.  LDS per block (reference message): 4 x 12.1 KB captures + 4.4 KB
 // table = 53 KB, three blocks = 12 waves (3 per SIMD) per CU.
-#ifndef FRAME_SYNC_WAVES
 #define FRAME_SYNC_WAVES 4
-#endif
 constexpr int SYM_THREADS = 256;    // frame_sym_kernel block: its items per block set the hand-off tile
 constexpr size_t FRAME_LDS_PER_CU = 160 * 1024;
 constexpr int SYNC_WAVES = FRAME_SYNC_WAVES;
@@ -389,18 +387,10 @@ constexpr int det_max_chunk() {
 }
 constexpr int DET_MAX_CHUNK = det_max_chunk();
 static_assert(64 * 2 * DET_MAX_CHUNK + 47 >= CAP_ABS_MAX, "two detection rounds cover every capture");
-#ifndef FRAME_ITEM_RUN
 #define FRAME_ITEM_RUN 4            // items per hand-out of the sync kernel's work counter (per wave)
-#endif
-#ifndef FRAME_LAZY
 #define FRAME_LAZY 1        // lazy capture + detection (see frame_sync_kernel; A/B: +5.3 %, profiles/r03/ab_n/)
-#endif
-#ifndef FRAME_R1_SPREAD
 #define FRAME_R1_SPREAD 1   // round 1 in one 16-position batch where spread chunks allow (A/B option)
-#endif
-#ifndef FRAME_LAZY_C0
 #define FRAME_LAZY_C0 31    // round-0 positions per lane when lazy (two 16-position batches)
-#endif
 // Detection geometry for Lc = cap_len - 47 positions: R rounds of 64 lanes, round 0 c0 positions per lane over
 // [0, B1 = 64 c0), round 1 c1 per lane from B1 (chunks odd: the lanes' LDS reads fall in distinct banks)
 struct DetGeom {
@@ -409,7 +399,6 @@ struct DetGeom {
     __host__ __device__ int r1_start(int l) const { return l * c1 + ((l * x1) >> 6); }
     __host__ __device__ static DetGeom of(int Lc) {
         DetGeom g{};
-#if FRAME_LAZY
         // Lazy: round 0 covers the first 64 FRAME_LAZY_C0 positions (the reference capture: 1984 of 2961), and
         // only the capture samples round 0 reads are generated before it; when round 0 alone decides
         // Packet_Selection and the matched filter reads inside that part, the rest of the capture and round 1
@@ -429,14 +418,6 @@ struct DetGeom {
                 g.x1 = r1;
             }
         }
-#else
-        // one round for the reference capture (chunk 47)
-        g.R = (Lc + 64 * DET_MAX_CHUNK - 1) / (64 * DET_MAX_CHUNK);
-        g.c0 = ((Lc + 64 * g.R - 1) / (64 * g.R)) | 1;
-        g.c1 = g.c0;
-        g.B1 = 64 * g.c0;
-        g.x1 = 0;
-#endif
         return g;
     }
     // the last capture sample (relative to the capture start) a detection round's register blocks load: every
@@ -487,28 +468,6 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// LDS conflict attribution probes (diagnostic builds only, tools/lds_attrib.py; results unchanged): FRAME_DUP_<SITE>
-// issues one access site's LDS instructions a second time, same instruction form and lane addresses, waited for at
-// once, so that the PMC deltas of SQ_INSTS_LDS / SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE against the plain build
-// are that site's instructions and their conflict and array cycles
-__device__ __forceinline__ void dup_read2_b32(const float *p) {
-    typedef float f2d __attribute__((ext_vector_type(2)));
-    f2d d;
-    asm volatile("ds_read2_b32 %0, %1 offset1:1\n\ts_waitcnt lgkmcnt(0)" : "=v"(d)
-                 : "v"((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float *)p));
-}
-__device__ __forceinline__ void dup_read_b32(const float *p) {
-    float d;
-    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(d)
-                 : "v"((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float *)p));
-}
-__device__ __forceinline__ void dup_write_b128(float *p, float4 v) {
-    typedef float f4d __attribute__((ext_vector_type(4)));
-    f4d d = {v.x, v.y, v.z, v.w};
-    asm volatile("ds_write_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" :: "v"((uint32_t)(uintptr_t)(__attribute__((address_space(3))) float *)p),
-                 "v"(d) : "memory");
-}
-
 // x mod the table period for 0 <= x < 2^14 (q = floor(x / period) by multiply-high: exact there)
 struct ImMod {
     int period;
@@ -525,18 +484,14 @@ struct ImMod {
 // (64 banks of 4 B, 2 LDS cycles per wave-instruction) and not a ds_read2_b32 (two 32-bank dword accesses, 4
 // cycles): the matched filter's lane starts are 10 floats apart, which puts lanes u and u + 16 on one bank of a
 // 32-bank dword access (2-way) and the runs of different needed ranges on further shared banks -- 7.7 conflict
-// cycles per ds_read2_b32 in the sync kernel (profiles/r05/lds_attrib.json, tools/ubench_lds_item.hip).
+// cycles per ds_read2_b32 in the sync kernel (profiles/r05/lds/lds_attrib_round4_kernel.json, tools/ubench_lds_item.hip).
 // FORM 0: float2 loads (the compiler pairs them into ds_read2_b32), 1: 8-byte vector loads (paired into
 // ds_read2_b64: two 16-lane accesses per half, 32 banks), 2: the same with a base VGPR per load so that they stay
 // single ds_read_b64 (A/B on the reference sweep, profiles/r05/ab/mf_load_forms.txt: 0 -> 1 +0.4 %, -> 2 +0.6 %,
 // conflict cycles 479 -> 351 per item).  The fixed-geometry kernel uses 2; the generic ones 1 (2 spills them at
 // their 168-VGPR budget).
-#ifndef FRAME_MF_B64
 #define FRAME_MF_B64 2
-#endif
-#ifndef FRAME_MF_B64_GEN
 #define FRAME_MF_B64_GEN 1
-#endif
 template <int ODD, int FORM, int N>
 __device__ __forceinline__ void lds_readn(const float *p, int s, float (&x)[N]) {
     static_assert(N & 1, "odd window");
@@ -585,9 +540,7 @@ __device__ __forceinline__ void capture_blocks(const A &a, int wave_len, float *
     const uint32_t pb = (uint32_t)(wave_len / (4 * FR_REPS)), nb_wave = (uint32_t)(wave_len / 4);
     uint32_t bm = (uint32_t)(bs + lane) % pb;
     const bool real = a.noise == OFDM_NOISE_REAL;        // real-only AWGN (D7), or noiseless
-#ifndef FRAME_CAP_U
 #define FRAME_CAP_U 4   // Philox blocks per lane per pass: the lazy capture's 8 + 4 blocks in passes of 4 (A/B: +1.3 % over 6, = 8)
-#endif
     // Passes are uniform over the wave and free of per-lane control flow: every lane loads, draws and combines
     // its FRAME_CAP_U blocks (a lane past `be` computes a block it does not store), so the blocks' Philox rounds
     // and Box-Muller transcendentals interleave (ILP 2 FRAME_CAP_U in the multiply chains)
@@ -622,16 +575,11 @@ __device__ __forceinline__ void capture_blocks(const A &a, int wave_len, float *
         for (int u = 0; u < FRAME_CAP_U; ++u)
             if (bb + 64 * u <= be) {
                 *reinterpret_cast<float4 *>(rbase + 4 * (bb + 64 * u - b0)) = v[u];
-#ifdef FRAME_DUP_CAP
-                dup_write_b128(rbase + 4 * (bb + 64 * u - b0), v[u]);
-#endif
             }
     }
 }
 
-#ifndef FRAME_SYNC_MINW
 #define FRAME_SYNC_MINW 3   // waves per SIMD the VGPR budget targets (LDS holds 3 blocks of 4 waves per CU)
-#endif
 // FIX_ND, FIX_CAP > 0: the launch geometry as compile-time constants -- n_data data symbols per frame, captures of
 // FIX_CAP samples generated from the waveform (no external capture, no dumps, no word-length statistics): the
 // reference message's sweep, with the detection rounds, table period, matched-filter runs and hand-off layout
@@ -686,10 +634,7 @@ __global__ __launch_bounds__(64 * W, FRAME_SYNC_MINW) void frame_sync_kernel(Fra
         // instead of being hoisted into SGPRs held across the item loop, which spill
         using KArgs = const __attribute__((address_space(4))) FrameArgs;
         KArgs *ap = (KArgs *)__builtin_amdgcn_kernarg_segment_ptr();
-#ifndef FRAME_FIX_OPAQUE
-#define FRAME_FIX_OPAQUE 1      // A/B option: 0 lets the fixed-geometry kernel hoist its arguments into SGPRs
-#endif
-        if (!FIX || FRAME_FIX_OPAQUE) asm volatile("" : "+s"(ap));
+        asm volatile("" : "+s"(ap));
         KArgs &a = *ap;
         // the geometry: compile-time constants (FIX), or re-read per item with the arguments
         const int n_data = FIX ? FIX_ND : a.n_data;
@@ -820,13 +765,6 @@ __global__ __launch_bounds__(64 * W, FRAME_SYNC_MINW) void frame_sync_kernel(Fra
                     constexpr int j = decltype(jc)::value;
 #pragma unroll
                     for (int k = 0; k < DET_B; ++k) { xr[j][k] = tr_[DET_B * j + k]; xi[j][k] = ti_[DET_B * j + k]; }
-#ifdef FRAME_DUP_DET
-#pragma unroll
-                    for (int k = 0; k < DET_B; k += 2) {
-                        dup_read2_b32((const float *)(tr_ + DET_B * j + k));
-                        dup_read2_b32((const float *)(ti_ + DET_B * j + k));
-                    }
-#endif
                 };
                 load_blk(std::integral_constant<int, 0>{});
                 load_blk(std::integral_constant<int, 1>{});
@@ -891,12 +829,6 @@ __global__ __launch_bounds__(64 * W, FRAME_SYNC_MINW) void frame_sync_kernel(Fra
             static_for<0, 2>([&](auto r2c) {
                 constexpr int r2 = decltype(r2c)::value;
                 if (r2 < R) {
-#ifdef FRAME_DUP_BP
-                    {
-                        int d;
-                        asm volatile("ds_bpermute_b32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(d) : "v"(owner * 4), "v"((int)(uint32_t)cm[r2]));
-                    }
-#endif
                     const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)cm[r2], owner, 64);
                     const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(cm[r2] >> 32), owner, 64);
                     if (rp == r2) w = ((unsigned long long)hi << 32) | lo;
@@ -1064,15 +996,6 @@ __global__ __launch_bounds__(64 * W, FRAME_SYNC_MINW) void frame_sync_kernel(Fra
                     const int si = im_mod(im0 + n_lo);
                     if (par_r) lds_readn<1, MF_FORM>(rbase, off + n_lo, xr); else lds_readn<0, MF_FORM>(rbase, off + n_lo, xr);
                     if (par_i) lds_readn<1, MF_FORM>(imt, si, xi); else lds_readn<0, MF_FORM>(imt, si, xi);
-#ifdef FRAME_DUP_MF
-#pragma unroll
-                    for (int m = 0; m < (MF_W - 1) / 2; ++m) {
-                        dup_read2_b32(rbase + off + n_lo + par_r + 2 * m);
-                        dup_read2_b32(imt + si + par_i + 2 * m);
-                    }
-                    dup_read_b32(rbase + off + n_lo + (par_r ? 0 : MF_W - 1));
-                    dup_read_b32(imt + si + (par_i ? 0 : MF_W - 1));
-#endif
 #pragma unroll
                     for (int o = 0; o < MF_RUN; ++o) {           // output at sample n_lo + 2 o + 20
                         if (s0 + o < e) {
@@ -1101,12 +1024,6 @@ __global__ __launch_bounds__(64 * W, FRAME_SYNC_MINW) void frame_sync_kernel(Fra
         // every fr[] sample the estimates read, loaded in one LDS round trip (lanes >= 16 read the coarse window
         // too, and drop it)
         const float2 cu = fr[80 + (lx & 15)], cw = fr[96 + (lx & 15)], l1 = fr[192 + lx], l2 = fr[256 + lx];
-#ifdef FRAME_DUP_CFO
-        dup_read2_b32((const float *)&fr[80 + (lx & 15)]);
-        dup_read2_b32((const float *)&fr[96 + (lx & 15)]);
-        dup_read2_b32((const float *)&fr[192 + lx]);
-        dup_read2_b32((const float *)&fr[256 + lx]);
-#endif
         float2 d0 = make_float2(0.f, 0.f), d1 = d0;          // the reference frame's data windows, for the hand-off
         if constexpr (FIX && FIX_ND == 2) {
             d0 = fr[336 + lx];
@@ -1207,9 +1124,7 @@ __global__ __launch_bounds__(64 * W, FRAME_SYNC_MINW) void frame_sync_kernel(Fra
 // message's items take 12 lanes, not 16).  The host picks dpq through the tile size a.ipb = 64 / quads per item
 // (sym_quads), from which the kernel derives it back.
 template <bool DUMP, int FIX_ND>   // DUMP: item 0's bits / subcarriers / metrics for ofdm_receiver
-#ifndef FRAME_SYM_MINB
 #define FRAME_SYM_MINB 2   // 3 waves/SIMD spills 196 VGPRs: frame mode 9 % slower
-#endif
 // FIX_ND > 0: n_data as a compile-time constant (the reference message's sweep: the hand-off offsets fold)
 __global__ __launch_bounds__(SYM_THREADS, FRAME_SYM_MINB) void frame_sym_kernel(FrameArgs a) {
     const int n_data = FIX_ND ? FIX_ND : a.n_data;
@@ -1237,10 +1152,8 @@ __global__ __launch_bounds__(SYM_THREADS, FRAME_SYM_MINB) void frame_sym_kernel(
         const bool dlane = item_ok && role >= r0 && dsym < n_data;
         const float2 *src = win_item(a.win, ipb, nw, item_ok ? i : base) + w;
         float2 x[64];
-#ifndef FRAME_SYM_GROUPS
 #define FRAME_SYM_GROUPS 2      // hand-off groups loaded per batch of first radix-4 stages (A/B: 2 +0.4 % over 1; 4
                                 // needs 172 VGPRs, 2 waves/SIMD, and gains nothing; profiles/r04/ab/x_ab_groups.txt)
-#endif
         // load fused with the first radix-4 stage, FRAME_SYM_GROUPS x 16 samples (hand-off groups) at a time
         // (fft() = DFT(x (-1)^n))
         static_for<0, 4>([&](auto gc) {
@@ -1388,12 +1301,8 @@ constexpr int LW_CHUNK = 31;
 constexpr int LW_ROUND = 64 * LW_CHUNK;              // 1,984 positions per round
 constexpr int LW_RES = 2 * LW_ROUND + 48;             // resident capture samples (rounds 0 and 1 and their windows)
 constexpr int LW_MAXP = 3;                            // matched-filter passes of 64 runs (33 + 13 nd <= 137 runs)
-#ifndef FRAME_LONG_MINW
 #define FRAME_LONG_MINW 2
-#endif
-#ifndef FRAME_MF_B64_LONG
 #define FRAME_MF_B64_LONG FRAME_MF_B64_GEN   // lds_readn form of the long kernel's matched filter
-#endif
 template <int W>
 __global__ __launch_bounds__(64 * W, FRAME_LONG_MINW) void frame_sync_long_kernel(FrameArgs a) {
     constexpr int SYNC_WAVES_L = W, SYNC_THREADS_L = 64 * W;
@@ -1839,9 +1748,7 @@ static int32_t word_bits(double mn, double mx) {
 // items per sync -> symbol hand-off: 2^22 items x 2 KB (reference message) = 8 GB of HBM, one launch pair per
 // 4M items (A/B, frame mode: 2^18 3.13e8, 2^20 3.33e8, 2^22 3.40e8 symbol-SNR/s -- each pair ends in a tail
 // and K4b' waits for K4b)
-#ifndef FRAME_CHUNK_LOG2
 #define FRAME_CHUNK_LOG2 22
-#endif
 constexpr int64_t FRAME_CHUNK_ITEMS = int64_t(1) << FRAME_CHUNK_LOG2;
 // items per chunk for n_data data symbols: 2^22, capped so that the hand-off buffer holds no more windows than the
 // reference message's 2^22 items do (1 + n_data windows of 512 B per item: 6 GiB; ADVICE r3: 8-symbol messages
@@ -1870,10 +1777,7 @@ static int run_frame_chunk(Ctx *c, FrameArgs &a) {
     a.im_period = a.ext ? (1 << 30) : a.wave_len / FR_REPS;
     a.im_magic = (uint32_t)((((uint64_t)1 << 32) + (uint64_t)a.im_period - 1) / (uint64_t)a.im_period);
     a.imt_len = (a.ext ? a.cap_len : a.im_period) + IMT_EXT;
-#ifndef FRAME_LDS_PAD
-#define FRAME_LDS_PAD 0     // A/B only: unused LDS per block, to measure K4b at lower occupancy
-#endif
-    const size_t lds = frame_lds_bytes(a.cap_len, a.n_data, a.n_snr, a.imt_len, a.word_stats) + FRAME_LDS_PAD;
+    const size_t lds = frame_lds_bytes(a.cap_len, a.n_data, a.n_snr, a.imt_len, a.word_stats);
     a.fr_in_cap = fr_in_capture(a.cap_len, a.n_data);
     a.region_floats = wave_region_floats(a.cap_len, a.n_data);
     if (!c->d_work) HIPOK(hipMalloc(&c->d_work, 256));
@@ -1909,7 +1813,7 @@ static int run_frame_chunk(Ctx *c, FrameArgs &a) {
     // profiles/r04/ab/h_frame8*.json; after the real-part table 4.28e8 against 4.50e8, and 4.15e8 with two-wave
     // blocks, ae_frame8_blocks.txt).  So one-wave blocks run only when they give every SIMD more waves:
     // resident = whole waves per SIMD x 4, from W x floor(LDS per CU / block LDS), at most 12
-    const size_t lds1 = frame_lds_bytes(a.cap_len, a.n_data, a.n_snr, a.imt_len, a.word_stats, 1) + FRAME_LDS_PAD;
+    const size_t lds1 = frame_lds_bytes(a.cap_len, a.n_data, a.n_snr, a.imt_len, a.word_stats, 1);
     auto resident = [](size_t b, int w) {
         return std::min<int64_t>(12, w * (int64_t)(FRAME_LDS_PER_CU / b) / 4 * 4);
     };

@@ -252,57 +252,6 @@ __device__ __forceinline__ void flush_lanes(const FrameAcc &acc, bool leader, un
     }
 }
 
-// ---- the same five slot terms reduced across the wave first (flush_lanes' 5 x 64 same-address
-// ds_add_u64 per SNR iteration serialise in the LDS pipe and count as bank conflicts).  Every lane's terms are
-// split into 32-bit words whose fields have room for the 64-lane sum, the words are summed by DPP (row sums, then
-// row_bcast 15 / 31: lane 63 holds the total), and lane 63 adds the five totals: 5 single-lane atomics.
-// Fields (per lane -> wave sum): ferr, fax <= 192 -> < 2^14; frame / finite flags -> <= 64; EVM_PRE_Q's low 32 bits
-// as two 16-bit halves -> < 2^22 (a lane whose EVM_PRE_Q reaches 2^32, i.e. sum |z - d|^2 >= 4096 -- low-SNR LS
-// frames -- sends the whole wave's EVM_PRE_Q through per-lane atomics instead); the dB terms biased by 2^29
-// (|EVM_dB| < 400 dB, so 0 < v + 2^29 < 2^30) as 15-bit halves -> < 2^21, the bias times the valid lanes taken
-// off again.  Integer sums throughout: the counters are bit-identical to flush_lanes'.
-__device__ __forceinline__ uint32_t wave_total_u32(uint32_t v) {
-    v += dpp_u<DPP_QUAD_XOR1>(v);
-    v += dpp_u<DPP_QUAD_XOR2>(v);
-    v += dpp_u<DPP_ROW_HALF_MIRROR>(v);
-    v += dpp_u<DPP_ROW_MIRROR>(v);                                                      // every lane: its row's sum
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);      // row_bcast:15 -> rows 1, 3
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);      // row_bcast:31 -> rows 2, 3
-    return v;                                                                           // lane 63: the wave's sum
-}
-
-__device__ __forceinline__ void flush_wave(float fe_pre, uint32_t ferr, uint32_t fax, bool valid, int lane,
-                                           unsigned long long *slots /*[5]*/) {
-    constexpr float K = 3.01029995663981195214f, L96 = 6.58496250072115618146f;    // frame_metrics' constants
-    constexpr int32_t BIAS = 1 << 29;
-    const uint64_t pre = (uint64_t)q20_nonneg(fe_pre);
-    const float lg = K * (__builtin_amdgcn_logf(fe_pre) - L96);
-    const int32_t dbpre = (int32_t)q20_db(fe_pre > 0.f ? fmaxf(lg, -400.0f) : -400.0f);
-    const int32_t dbpost = fax > 0u ? (int32_t)q20_db(K * (__builtin_amdgcn_logf((float)fax) + (1.0f - L96))) : 0;
-    const uint32_t m = valid ? 0xffffffffu : 0u;
-    const uint32_t plo = (uint32_t)pre;
-    const bool big = valid && (uint32_t)(pre >> 32) != 0u;
-    const bool any_big = __ballot(big) != 0ull;                // wave-uniform: rare (low-SNR LS frames)
-    const uint32_t pm = any_big ? 0u : m;
-    const uint32_t ub = (uint32_t)(dbpre + BIAS), uo = (uint32_t)(dbpost + BIAS);
-    const uint32_t w0 = wave_total_u32((ferr | (fax << 16)) & m);
-    const uint32_t w1 = wave_total_u32(((plo & 0xffffu) & pm) | ((min(ferr, 1u) << 22) & m));
-    const uint32_t w2 = wave_total_u32(((plo >> 16) & pm) | ((min(fax, 1u) << 22) & m));
-    const uint32_t w3 = wave_total_u32((ub & 0x7fffu) & m);
-    const uint32_t w4 = wave_total_u32((ub >> 15) & m);
-    const uint32_t w5 = wave_total_u32((uo & 0x7fffu) & m);
-    const uint32_t w6 = wave_total_u32((uo >> 15) & m);
-    if (any_big && valid) atomicAdd(&slots[2], (unsigned long long)pre);
-    const int64_t nb = (int64_t)__popcll(__ballot(valid)) * BIAS;      // (ballot outside the one-lane branch)
-    if (lane == 63) {
-        atomicAdd(&slots[0], (unsigned long long)(w0 & 0xffffu) | ((unsigned long long)(w0 >> 16) << 32));
-        atomicAdd(&slots[1], (unsigned long long)(w1 >> 22) | ((unsigned long long)(w2 >> 22) << 32));
-        if (!any_big) atomicAdd(&slots[2], (unsigned long long)(w1 & 0x3fffffu) + ((unsigned long long)(w2 & 0x3fffffu) << 16));
-        atomicAdd(&slots[3], (unsigned long long)((int64_t)w3 + ((int64_t)w4 << 15) - nb));
-        atomicAdd(&slots[4], (unsigned long long)((int64_t)w5 + ((int64_t)w6 << 15) - nb));
-    }
-}
-
 // term k of an SNR point's LDS slots -> (counter index, value)
 __device__ __forceinline__ int slot_term(const unsigned long long *s, int k, unsigned long long &v) {
     switch (k) {

@@ -19,18 +19,8 @@
 #include "ofdm_internal.h"
 #include "ofdm_rxcommon.h"
 
-#ifndef OFDM_PACK_SPLITD            // LS AWGN: data windows as two 32-point real FFTs (see the SNR loop)
-#define OFDM_PACK_SPLITD 0
-#endif
-#ifndef OFDM_RX_PACK_WAVES          // waves per SIMD the LS receiver is register-budgeted for
-#define OFDM_RX_PACK_WAVES (OFDM_PACK_SPLITD ? 3 : 2)
-#endif
-#ifndef OFDM_PACK_SPLIT_PF          // split loop: bin-pair LDS operands loaded this many pairs ahead
-#define OFDM_PACK_SPLIT_PF 1
-#endif
-#ifndef OFDM_RX_PACK_IDEAL_WAVES    // the ideal-CSI receiver (no LTF spectrum) fits 168 VGPRs / 53 KB LDS
-#define OFDM_RX_PACK_IDEAL_WAVES 3
-#endif
+#define OFDM_RX_PACK_WAVES 2          // waves per SIMD the LS receiver is register-budgeted for
+#define OFDM_RX_PACK_IDEAL_WAVES 3    // the ideal-CSI receiver (no LTF spectrum) fits 168 VGPRs / 53 KB LDS
 
 namespace ofdm {
 
@@ -42,21 +32,15 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) const f4v lcf4;
 typedef unsigned int u2v __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) const u2v lcu2;
-typedef __attribute__((address_space(3))) const uint32_t lcu1;
 typedef __attribute__((address_space(3))) f2v lf2;
 
-// the LTF noise spectrum E'[k] of the odd-k pairs waits in LDS (per wave) until the odd sub-blocks are
-// consumed: 22 VGPRs less at the register peak (the data FFT's 128 + the even pairs' E')
-#ifndef OFDM_PACK_PF
 // LS AWGN receiver: bin-pair LDS operands loaded this many pairs ahead (A/B, profiles/r03/ab_i: c3 +1.2 % at 2,
 // +0.6 % at 1; the Rayleigh receiver, whose E spectrum is per frame, gains nothing and keeps 0)
-#define OFDM_PACK_PF 2
-#endif
-#ifndef OFDM_PACK_EE_LDS
-#define OFDM_PACK_EE_LDS 24   // 24 = none: no spill without it (222 VGPRs); A/B option
-#endif
-constexpr int EE_LDS_FIRST = OFDM_PACK_EE_LDS;     // pairs >= this one are parked in LDS
-constexpr int EE_LDS_N = PACK_PAIRS - EE_LDS_FIRST;
+constexpr int PACK_PF = 2;
+// the data windows' noise generation: a scheduling fence after every PACK_GEN_SPLIT Philox quarters
+constexpr int PACK_GEN_SPLIT = 2;
+// the bin-pair loop: a scheduling fence after every PACK_FENCE_PAIRS pairs (keeps the PF loads where written)
+constexpr int PACK_FENCE_PAIRS = 2;
 
 // 16-point digit reversal (dif4<16> output order): bin m of a 16-point sub-transform at position rev16(m)
 __host__ __device__ constexpr int rev16(int m) { return ((m & 3) << 2) | (m >> 2); }
@@ -90,9 +74,6 @@ __device__ __forceinline__ void chan_pairs(const float2 (&h)[4], float4 *col) {
 
 // Group prologue: clean spectrum of symbol `s` (window rows 16..79 of the Tx batch, times (-1)^n for
 // fft(), OFDM.c:314-318) -> the 24 bin pairs (C[k], C[64 - k]) of spec[p][half][frame].
-// EARLY: each sub-block's pairs are stored as soon as they are final (sub-block 0, 2, then 1 + 3), which
-// lowers the register peak of the 168-VGPR split receiver's prologue.
-template <bool EARLY = false>
 __device__ __forceinline__ void clean_spectrum(const RxArgs &a, int64_t s, float4 *spec_col /* &spec[0][half][f] */) {
     gcf2 *src = (gcf2 *)(a.tx + 16 * a.pitch + s);
     int P = (int)a.pitch;
@@ -116,20 +97,8 @@ __device__ __forceinline__ void clean_spectrum(const RxArgs &a, int64_t s, float
         const float2 c0 = x[digit_rev4(k)], c1 = x[digit_rev4(64 - k)];
         spec_col[p * 2 * PK_FRAMES] = make_float4(c0.x, c0.y, c1.x, c1.y);
     };
-    if constexpr (EARLY) {
-        dif_sub16<false, 0>(x);
-        static_for<0, 6>(store);
-        sched_fence();
-        dif_sub16<false, 2>(x);
-        static_for<6, 13>(store);
-        sched_fence();
-        dif_sub16<false, 1>(x);
-        dif_sub16<false, 3>(x);
-        static_for<13, PACK_PAIRS>(store);
-    } else {
-        static_for<0, 4>([&](auto rc) { dif_sub16<false, decltype(rc)::value>(x); });
-        static_for<0, PACK_PAIRS>(store);
-    }
+    static_for<0, 4>([&](auto rc) { dif_sub16<false, decltype(rc)::value>(x); });
+    static_for<0, PACK_PAIRS>(store);
 }
 
 // Per-bin demap of one data symbol at one bin: u = Z / g with g > 0 (KIND 0: g = 1, KIND 2: g = 2r),
@@ -164,32 +133,14 @@ __device__ __forceinline__ void demap_bin(float2 u, float r, uint32_t &t, uint32
     }
 }
 
-// Ablation builds (diagnostics only, results are wrong; their run time against the real kernel prices a
-// stage including its stalls): OFDM_ABL_NO_PHILOX replaces the Philox rounds by one multiply,
-// OFDM_ABL_NO_BM the Box-Muller transcendentals by multiplies, OFDM_ABL_NO_PREPASS transforms the clean
-// symbols of a block's first group only.  For the per-stage instruction budget of the SNR loop (tools/stage_mix.py,
-// static counts of the assembly): OFDM_ABL_NO_DFFT drops the data windows' 64-point FFT (the noise samples go to
-// the bin pairs untransformed), OFDM_ABL_NO_LFFT the LTF pair's 32-point FFT, OFDM_ABL_NO_EQ replaces each bin
-// pair's estimate / equaliser / slicer / demap by one sum, OFDM_ABL_NO_CNT drops frame_metrics + the LDS flush.
+// (The ablation builds that priced each stage, OFDM_ABL_* -- tools/stage_mix.py's per-stage budget of the SNR loop
+// -- are in git history: profiles/r06/README.md.)
 template <typename KS>
 __device__ __forceinline__ Noise4 pack_noise(const PhiloxHead &hd, uint32_t c2, const KS &keys, uint32_t k1, float K) {
-#ifdef OFDM_ABL_NO_PHILOX
-    (void)keys; (void)k1;
-    const uint64_t p = (uint64_t)PHILOX_M1 * (c2 ^ hd.n2);
-    const uint4 o = make_uint4((uint32_t)p, (uint32_t)(p >> 32), (uint32_t)p ^ hd.c3, (uint32_t)(p >> 32) ^ hd.c1);
-#else
     uint4 o;
     if constexpr (std::is_same_v<KS, PhiloxKeysV>) o = philox10_c2(hd, c2, keys);
     else o = philox10_c2(hd, c2, keys, k1);
-#endif
-#ifdef OFDM_ABL_NO_BM
-    Noise4 n;
-    n.r0 = K * (float)o.x; n.r1 = K * (float)o.z;
-    n.c0 = (float)o.y; n.s0 = n.c0 * 0.5f; n.c1 = (float)o.w; n.s1 = n.c1 * 0.5f;
-    return n;
-#else
     return noise4_of(o, K);
-#endif
 }
 
 #ifdef OFDM_PACK_STAMPS   // diagnostic build: s_memtime per item phase, per wave role, summed over the grid
@@ -210,53 +161,21 @@ static __device__ unsigned long long g_pack_stamps[4][8];
 // CHAN (KIND 2 only): OFDM_CHAN_RAYLEIGH4 applies each frame's 4-tap channel to its clean spectra in the
 // group prologue (chan_bin): it does not depend on the SNR point, and the real noise is added after the
 // channel (OFDM.c:651 order), so the SNR loop is the AWGN loop with a per-frame E spectrum `fce`.
-#ifndef OFDM_RX_PACK_FADE_WAVES     // the Rayleigh LS receiver (72 KB of LDS: two blocks per CU)
 #define OFDM_RX_PACK_FADE_WAVES 2
-#endif
-#ifndef PACK_SACC_SUB_LS
 #define PACK_SACC_SUB_LS 4  // copies of the block's SNR accumulators, LS receivers (see sacc; at most 4 for the
                             // Rayleigh one, whose two blocks per CU leave room for no more).  A/B (round 4,
                             // profiles/r04/ab): c3 1.236 -> 1.260e10, c5 1.193 -> 1.220e10; 8 copies the same
-#endif
-#ifndef OFDM_PACK_SPEC_LIN
-// A/B option: the prologue's clean-spectrum stores with a wave's lanes on consecutive frames (conflict-free LDS
-// stores, but each wave then reads every other symbol of the Tx rows): c3 -4.7 %, c5 -4 %, c2 +-0 (round 4,
-// profiles/r04/ab/ab_map.txt), so the 2-way store conflicts stay
-#define OFDM_PACK_SPEC_LIN 0
-#endif
-#ifndef PACK_SACC_SUB
 #define PACK_SACC_SUB 1     // the same for the ideal-CSI receiver (2 copies spill it at its 168-VGPR budget)
-#endif
-// A/B options: the SNR iteration's five counter terms wave-reduced by DPP and added by one lane (flush_wave,
-// ofdm_rxcommon.h) instead of 64 same-address LDS atomics per term (flush_lanes).  Negative (round 5,
-// profiles/r05/ab/wave_flush.txt): c2 -5.2 %, c3 -7.0 %, c5 -1.1 % -- the serialised atomics run in the LDS pipe
-// beside the VALU stream, the ~70 VALU of the reduction do not
-#ifndef OFDM_PACK_WAVE_FLUSH_IDEAL
-#define OFDM_PACK_WAVE_FLUSH_IDEAL 0
-#endif
-#ifndef OFDM_PACK_WAVE_FLUSH_LS
-#define OFDM_PACK_WAVE_FLUSH_LS 0
-#endif
+// (Wave-reducing the SNR iteration's five counter terms by DPP instead of the 64 same-address LDS atomics per term
+// measured negative, round 5, profiles/r05/ab/wave_flush.txt: c2 -5.2 %, c3 -7.0 %, c5 -1.1 % -- the serialised
+// atomics run in the LDS pipe beside the VALU stream, the ~70 VALU of the reduction do not.)
 template <int KIND, int CONV, int CHAN, bool DUMP>
 __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFDM_RX_PACK_FADE_WAVES : OFDM_RX_PACK_WAVES)
                                             : OFDM_RX_PACK_IDEAL_WAVES) void rx_pack_kernel(RxArgs a) {
     constexpr bool FADE = CHAN == OFDM_CHAN_RAYLEIGH4;
     static_assert(!FADE || KIND == 2, "the packed Rayleigh receiver is the LS one");
-    // LS AWGN, split data windows: D0 and D1 each through a 32-point FFT of its even/odd samples (the LTF
-    // pair's transform), demapped pass by pass, instead of d0 + j d1 through one 64-point FFT: the E
-    // spectrum (48 VGPRs) is then live beside 64 VGPRs of transform instead of 128
-    constexpr bool SPLIT = KIND == 2 && !FADE && OFDM_PACK_SPLITD;
-    constexpr bool EEL = KIND == 2 && EE_LDS_N > 0;
-    static_assert(!(SPLIT && EEL), "the split loop keeps the whole E spectrum in VGPRs");
-#ifndef OFDM_NO_PACK_WARM_LATE
-#ifndef OFDM_PACK_WLATE_FADE
-#define OFDM_PACK_WLATE_FADE 0      // A/B option: the late warm-up in the Rayleigh LS receiver too
-#endif
     // where the next item's L2 warm-up is issued (see the SNR loop)
-    constexpr bool WLATE = KIND == 2 && (!FADE || OFDM_PACK_WLATE_FADE);
-#else
-    constexpr bool WLATE = false;
-#endif
+    constexpr bool WLATE = KIND == 2 && !FADE;
     __shared__ __attribute__((aligned(16))) float4 spec[PACK_PAIRS][2][PK_FRAMES];   // 48 KB: (C[k], C[64-k])
     __shared__ __attribute__((aligned(16))) float4 ce[PACK_PAIRS];                   // LS: FFT((-1)^n 2T[n])
     __shared__ __attribute__((aligned(16))) float4 fce[FADE ? PACK_PAIRS : 1][FADE ? PK_FRAMES : 1];  // 24 KB: H' FFT(2T)
@@ -264,9 +183,8 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
     // flush_lanes' five slots per SNR point; for the first SACC_XQ points SUBN - 1 more copies: lane l adds into
     // copy l % SUBN, so that an SNR iteration's 5 x 64 same-address LDS atomics (the kernel's LDS bank-conflict
     // cycles) spread over SUBN addresses in distinct banks; the copies are summed before the flush
-    constexpr bool WFLUSH = KIND == 2 ? OFDM_PACK_WAVE_FLUSH_LS : OFDM_PACK_WAVE_FLUSH_IDEAL;
-    constexpr int SUBN = WFLUSH ? 1 : KIND != 2 ? PACK_SACC_SUB : FADE ? (PACK_SACC_SUB_LS < 4 ? PACK_SACC_SUB_LS : 4)
-                                                                  : PACK_SACC_SUB_LS;
+    constexpr int SUBN = KIND != 2 ? PACK_SACC_SUB : FADE ? (PACK_SACC_SUB_LS < 4 ? PACK_SACC_SUB_LS : 4)
+                                                      : PACK_SACC_SUB_LS;
     constexpr int SACC_XQ = 16;
     __shared__ unsigned long long sacc[OFDM_MAX_SNR][5];
     __shared__ unsigned long long sacx[SUBN > 1 ? SACC_XQ : 1][SUBN > 1 ? 5 * (SUBN - 1) : 1];
@@ -275,7 +193,9 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
         return SUBN > 1 && c > 0 && q < SACC_XQ ? &sacx[q][5 * (c - 1)] : sacc[q];
     };
     __shared__ uint32_t pf_dummy[64];                             // L2 warm-up destination (never read)
-    __shared__ __attribute__((aligned(8))) float2 eel[EEL ? 4 : 1][EEL ? EE_LDS_N : 1][EEL ? 64 : 1];
+    // 8 B of LDS that a pruned option's array held in every measured build (round 6, profiles/r06/README.md): kept,
+    // with its per-iteration address, so that the code objects stay byte-identical to the PMC-certified builds
+    __shared__ __attribute__((aligned(8))) float2 lds_keep[1];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);      // wave-uniform: the SNR loop runs on SGPRs
 #ifdef OFDM_PACK_STAMPS
@@ -305,13 +225,6 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
             }
         }
     }
-#ifdef OFDM_PACK_VKEYS          // A/B: round keys in VGPRs (fast-class v_bitop3): +0.3 % c3, 20 VGPRs
-    PhiloxKeysV vkeys;
-    vkeys.init(a.k0, a.k1);
-#define PKEYS vkeys, 0u
-#else
-#define PKEYS a.k0, a.k1
-#endif
     const int64_t n_groups = (a.n_frames + PK_FRAMES - 1) / PK_FRAMES;
     // Work items: the groups of the full rounds (every block takes gridDim.x-strided groups, all SNR points),
     // then the T tail groups with their SNR points split S ways over up to S T <= gridDim.x blocks, so the
@@ -319,11 +232,7 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
     // integer sums: the split does not change them.
     // (32-bit item arithmetic: a launch holds at most 2^23 frames = 2^17 groups)
     const int B = (int)gridDim.x, G = (int)n_groups, R = G / B, T = G - R * B;
-#ifndef OFDM_PACK_NO_TAIL_SPLIT
     const int S = T > 0 ? max(1, min(4, B / T)) : 1;
-#else
-    const int S = 1;
-#endif
     const int n_items = R * B + T * S;
     // Items past the first gridDim.x are handed out one at a time from a.work: during an item's prologue
     // thread 128 fetches the block's next item and wave 2 warms L2 with that item's Tx rows.  Blocks that
@@ -339,7 +248,7 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
         PK_STAMP(0);                                       // item-top barrier (waiting for the other waves)
         // group-invariant addresses are re-derived from the thread index here, not held across the SNR
         // loop (they would be the only values spilled)
-        int t = SPLIT ? (wv << 6) + lane_fresh() : tid;
+        int t = tid;
         opaque(t);
         // kernel arguments read where used through an opaque kernarg pointer: hoisted, the 40 words of each
         // TxArgs would be held in SGPRs across the item loop and spill
@@ -361,19 +270,8 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
             }
             __syncthreads();
         }
-#ifdef OFDM_ABL_NO_PREPASS
-        if (t < PK_SYMS && grp == blockIdx.x) {
-#else
         if (t < PK_SYMS) {
-#endif
-#if OFDM_PACK_SPEC_LIN
-            // thread t: symbol 2 f + d of the group with d = t / 64, f = t % 64, so that a wave's 64 lanes store
-            // 64 consecutive frames' pairs (conflict-free ds_write_b128; with symbol t per thread, lanes t and
-            // t + 1 stored to the two halves, 1 KB apart, on the same banks: 2-way conflicts on every store)
-            clean_spectrum<SPLIT>(a, grp * PK_SYMS + 2 * (t & 63) + (t >> 6), &spec[0][t >> 6][t & 63]);
-#else
-            clean_spectrum<SPLIT>(a, grp * PK_SYMS + t, &spec[0][t & 1][t >> 1]);
-#endif
+            clean_spectrum(a, grp * PK_SYMS + t, &spec[0][t & 1][t >> 1]);
         } else {
             const int j = t - PK_SYMS;
             const uint32_t *src = a.bits + 7 * a.pitch + grp * PK_SYMS + j;
@@ -381,15 +279,10 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
             truth[1][j] = src[a.pitch];
             truth[2][j] = src[2 * a.pitch];
             if (j < 64) {                                  // wave 2: the next item
-#ifndef OFDM_PACK_STATIC_ITEMS
                 int nx = 0;
                 if (j == 0) nx = B + (int)atomicAdd(a.work, 1ull);
                 nx = __builtin_amdgcn_readlane(nx, 0);          // lane 0 (j == 0) fetched it
-#else
-                const int nx = w + B;
-#endif
                 if (j == 0) next_item = nx;
-#ifndef OFDM_PACK_NO_L2_WARM
                 // warm L2 with the next item's group (64 rows x 1 KB: one 4-byte LDS-DMA read per 128-B
                 // line, into a dummy LDS word), so the next prologue's loads hit L2 instead of HBM (not when
                 // the launch builds its own batch: those rows are written by the next item itself)
@@ -403,7 +296,6 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
                                                          (__attribute__((address_space(3))) void *)pf_dummy, 4, 0, 0);
                     }
                 }
-#endif
             }
             // the next chunk's Tx batch (ofdm_set_next_tx), one symbol per lane: group gg of this launch's
             // sub-0 item builds the next batch's symbols [128 gg', 128 gg' + 128) for gg' = gg, gg + G, ...
@@ -442,7 +334,7 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
             __syncthreads();
         }
         PK_STAMP(3);                                       // Rayleigh: faded spectra
-        const int64_t fl = grp * PK_FRAMES + (SPLIT ? lane_fresh() : lane);
+        const int64_t fl = grp * PK_FRAMES + lane;
         const bool valid = fl < a.n_frames;
         const uint64_t f = a.first_frame + (uint64_t)fl;
         for (int q = wv + 4 * sub; q < a.n_snr; q += 4 * ns) {
@@ -456,7 +348,7 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
                     KArgsW *apw = (KArgsW *)__builtin_amdgcn_kernarg_segment_ptr();
                     if (nx < n_items && apw->own.n_sym == 0) {
                         const int64_t ng = nx < R * B ? nx : R * B + (nx - R * B) / S;
-                        const int ln = SPLIT ? lane_fresh() : lane;     // split: nothing lane-derived held
+                        const int ln = lane;
 #pragma unroll
                         for (int i = 0; i < 8; ++i) {
                             const int line = ln + 64 * i;                      // 0..511
@@ -476,8 +368,8 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
             // z[m] = e'[2m] + j e'[2m+1] with e'[n] = (-1)^n e[n]; radix-2 stage fused, then two dif4<16>
             float2 z[64];      // z[0..31] used
             float2 ee[PACK_PAIRS];
-            lf2 *eew = (lf2 *)&eel[EEL ? wv : 0][0][EEL ? lane : 0];
-            opaque(eew);
+            lf2 *keep = (lf2 *)&lds_keep[0];
+            opaque(keep);
             if constexpr (KIND == 2) {
                 const float KE = noise_k(sigma * 1.41421356237309504880f);
                 static_for<0, 4>([&](auto ic) {
@@ -485,40 +377,26 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
                     uint32_t tg = 48u + 2 * i;
                     opaque(tg);
                     // blocks b = 2i, 2i+1 (z[4i..4i+3]) and b + 8 (z[4i+16..4i+19])
-#ifdef OFDM_PACK_VK4       // A/B: the four blocks' rounds together, round keys in 2 VGPRs advanced per round
-                    uint4 o4[4];
-                    const uint32_t c2s[4] = {tg, tg + 8, tg + 1, tg + 9};
-                    philox10_c2_vk<4>(hd, c2s, a.k0, a.k1, o4);
-#endif
                     static_for<0, 2>([&](auto hc) {
                         constexpr int h = decltype(hc)::value;
-#ifdef OFDM_PACK_VK4
-                        const Noise4 lo = noise4_of(o4[2 * h], KE);
-                        const Noise4 hi = noise4_of(o4[2 * h + 1], KE);
-#else
-                        const Noise4 lo = pack_noise(hd, tg + h, PKEYS, KE);
-                        const Noise4 hi = pack_noise(hd, tg + 8 + h, PKEYS, KE);
-#endif
+                        const Noise4 lo = pack_noise(hd, tg + h, a.k0, a.k1, KE);
+                        const Noise4 hi = pack_noise(hd, tg + 8 + h, a.k0, a.k1, KE);
                         constexpr int m = 4 * i + 2 * h;
                         z[m] = make_float2(lo.r0 * lo.c0, -(lo.r0 * lo.s0));
                         z[m + 1] = make_float2(lo.r1 * lo.c1, -(lo.r1 * lo.s1));
                         z[m + 16] = make_float2(hi.r0 * hi.c0, -(hi.r0 * hi.s0));
                         z[m + 17] = make_float2(hi.r1 * hi.c1, -(hi.r1 * hi.s1));
                     });
-#ifndef OFDM_ABL_NO_LFFT
                     static_for<0, 4>([&](auto jc) {
                         constexpr int j = 4 * i + decltype(jc)::value;
                         const float2 u = z[j], v = z[j + 16];
                         z[j] = cadd(u, v);
                         z[j + 16] = twiddle<2 * j, false>(csub(u, v));     // W32^j
                     });
-#endif
                     sched_fence();
                 });
-#ifndef OFDM_ABL_NO_LFFT
                 dif4<false, 16, 0>(z);
                 dif4<false, 16, 16>(z);
-#endif
                 // E'[k] = (Z[k] + conj Z[-k]) / 2 - j W64^k (Z[k] - conj Z[-k]) / 2 (Z indices mod 32), kept
                 // as 2 E'[k] per pair (48 VGPRs instead of the 62 of Z); E'[64 - k] = conj E'[k]
                 static_for<0, PACK_PAIRS>([&](auto pc) {
@@ -527,117 +405,10 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
                     const float2 P = z[pos32(k)], Qv = z[pos32(32 - k)];
                     const float2 F = make_float2(P.x + Qv.x, P.y - Qv.y);
                     const float2 H = twiddle<k, false>(make_float2(P.x - Qv.x, P.y + Qv.y));
-                    if constexpr (p < EE_LDS_FIRST) {
-                        ee[p] = make_float2(F.x + H.y, F.y - H.x);
-                    } else {
-                        f2v v; v.x = F.x + H.y; v.y = F.y - H.x;
-                        eew[(p - EE_LDS_FIRST) * 64] = v;
-                    }
+                    ee[p] = make_float2(F.x + H.y, F.y - H.x);
                 });
                 sched_fence();
             }
-            if constexpr (SPLIT) {
-                // ---- data window D (D0 at t = 336 + n, Philox block 84 + n/4; D1 at t = 416 + n, block 104 + n/4)
-                // packed as z[m] = e'[2m] + j e'[2m+1], e'[n] = (-1)^n d[n], through the LTF pair's 32-point
-                // transform; per bin pair 2 N[k] = (Z[k] + conj Z[-k]) - j W64^k (Z[k] - conj Z[-k]), then the
-                // clean spectrum, the LS estimate (S and 1/|S|^2 recomputed in each pass), ZF and the demap
-                const float K = noise_k(sigma);
-                float evm = 0.f;
-                uint32_t em = 0u, be = 0u, ax = 0u, t = 0u;
-                uint32_t sm;
-                asm volatile("v_mov_b32 %0, 0x80000000" : "=v"(sm));
-                const int ln = lane_fresh();
-                lcf4 *sp = (lcf4 *)&spec[0][0][ln];
-                lcu1 *tw = (lcu1 *)&truth[0][2 * ln];
-                opaque(sp); opaque(tw);
-                static_for<0, 2>([&](auto Dc) {
-                    constexpr int D = decltype(Dc)::value;
-                    static_for<0, 4>([&](auto ic) {
-                        constexpr int i = decltype(ic)::value;
-                        uint32_t tg = 84u + 20u * D + 2 * i;
-                        opaque(tg);
-                        static_for<0, 2>([&](auto hc) {
-                            constexpr int h = decltype(hc)::value;
-                            const Noise4 lo = pack_noise(hd, tg + h, PKEYS, K);
-                            const Noise4 hi = pack_noise(hd, tg + 8 + h, PKEYS, K);
-                            constexpr int m = 4 * i + 2 * h;
-                            z[m] = make_float2(lo.r0 * lo.c0, -(lo.r0 * lo.s0));
-                            z[m + 1] = make_float2(lo.r1 * lo.c1, -(lo.r1 * lo.s1));
-                            z[m + 16] = make_float2(hi.r0 * hi.c0, -(hi.r0 * hi.s0));
-                            z[m + 17] = make_float2(hi.r1 * hi.c1, -(hi.r1 * hi.s1));
-                        });
-                        static_for<0, 4>([&](auto jc) {
-                            constexpr int j = 4 * i + decltype(jc)::value;
-                            const float2 u = z[j], v = z[j + 16];
-                            z[j] = cadd(u, v);
-                            z[j + 16] = twiddle<2 * j, false>(csub(u, v));
-                        });
-                        sched_fence();
-                    });
-                    float2 *deq = nullptr;
-                    uint32_t *dbit = nullptr;
-                    if constexpr (DUMP) {
-                        if (valid) {
-                            const int64_t r0 = ((int64_t)q * a.dump_frames + fl) * 2 + D;
-                            deq = a.dump_eq + r0 * 48;
-                            dbit = a.dump_bits + r0 * 3;
-                        }
-                    }
-                    uint32_t db[3] = {0u, 0u, 0u};
-                    constexpr int PF = OFDM_PACK_SPLIT_PF;
-                    f4v pcs[PF + 1];
-                    float4 pe4[PF + 1];
-                    auto load_pair = [&](auto pc) {
-                        constexpr int p = decltype(pc)::value;
-                        if constexpr (p < PACK_PAIRS) {
-                            pcs[p % (PF + 1)] = sp[(p * 2 + D) * PK_FRAMES];
-                            pe4[p % (PF + 1)] = ce[p];
-                        }
-                    };
-                    static_for<0, PF + 1>(load_pair);
-                    auto pair = [&](auto pc) {
-                        constexpr int p = decltype(pc)::value;
-                        constexpr int k = pair_bin(p), k2 = 64 - k;
-                        if constexpr ((p & 7) == 0) t = tw[(p >> 3) * PK_SYMS + D];
-                        const f4v c = pcs[p % (PF + 1)];
-                        const float4 e4 = pe4[p % (PF + 1)];
-                        load_pair(std::integral_constant<int, p + PF + 1>{});
-                        const float2 P = z[pos32(k)], Qv = z[pos32(32 - k)];
-                        const float2 F = make_float2(P.x + Qv.x, P.y - Qv.y);
-                        const float2 H = twiddle<k, false>(make_float2(P.x - Qv.x, P.y + Qv.y));
-                        const float2 V = make_float2(F.x + H.y, F.y - H.x);          // 2 N[k]
-                        const float2 yk = make_float2(fmaf(0.5f, V.x, c.x), fmaf(0.5f, V.y, c.y));
-                        const float2 ym = make_float2(fmaf(0.5f, V.x, c.z), fmaf(-0.5f, V.y, c.w));
-                        const float2 Sk = make_float2(fmaf(0.5f, ee[p].x, e4.x), fmaf(0.5f, ee[p].y, e4.y));
-                        const float2 Sm = make_float2(fmaf(0.5f, ee[p].x, e4.z), fmaf(-0.5f, ee[p].y, e4.w));
-                        const float rk = __builtin_amdgcn_rcpf(fmaf(Sk.x, Sk.x, Sk.y * Sk.y));
-                        const float rm = __builtin_amdgcn_rcpf(fmaf(Sm.x, Sm.x, Sm.y * Sm.y));
-                        const float2 uk = cscale(cmulc(yk, Sk), (float)ltf_sign(k));
-                        const float2 um = cscale(cmulc(ym, Sm), (float)ltf_sign(k2));
-                        demap_bin<2, DUMP>(uk, rk, t, sm, evm, em, data_index(k), deq, db);
-                        demap_bin<2, DUMP>(um, rm, t, sm, evm, em, data_index(k2), deq, db);
-                        if constexpr ((p & 7) == 7) {
-                            ax += __popc(em);
-                            be += __popc(em & 0x55555555u) + __popc((em ^ (em >> 1)) & 0x55555555u);
-                            em = 0u;
-                        }
-                        opaque(evm);
-                        if constexpr ((p & 1) == 1) sched_fence();
-                    };
-                    dif4<false, 16, 0>(z);
-                    static_for<0, 13>(pair);      // even k: the first 16-point sub-transform
-                    sched_fence();
-                    dif4<false, 16, 16>(z);
-                    static_for<13, PACK_PAIRS>(pair);
-                    if constexpr (DUMP) {
-                        if (dbit) { dbit[0] = db[0]; dbit[1] = db[1]; dbit[2] = db[2]; }
-                    }
-                    sched_fence();
-                });
-                FrameAcc acc;
-                frame_metrics(acc, 4.0f * evm, be, ax);
-                flush_lanes(acc, valid, slots(q, lane));
-            } else {
             // ---- data windows: x[n] = (-1)^n (d0[n] + j d1[n]) fused with the first radix-4 stage.
             // Gaussian t of the frame's stream is sample t of the frame timeline: D0 at
             // t = 336 + n (Philox block 84 + n/4), D1 at t = 416 + n (block 104 + n/4).
@@ -647,36 +418,19 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
                 constexpr int g = decltype(gc)::value;
                 uint32_t tg = 84u + g;
                 opaque(tg);
-#ifdef OFDM_PACK_VK4
-                uint4 o4[4];
-#endif
                 static_for<0, 4>([&](auto Qc) {
                     constexpr int Q = decltype(Qc)::value;
-#ifdef OFDM_PACK_VK4
-                    if constexpr ((Q & 1) == 0) {
-                        const uint32_t c2s[4] = {tg + 4 * Q, tg + 20 + 4 * Q, tg + 4 * Q + 4, tg + 24 + 4 * Q};
-                        philox10_c2_vk<4>(hd, c2s, a.k0, a.k1, o4);
-                    }
-                    const Noise4 n0 = noise4_of(o4[2 * (Q & 1)], K);
-                    const Noise4 n1 = noise4_of(o4[2 * (Q & 1) + 1], K);
-#else
-                    const Noise4 n0 = pack_noise(hd, tg + 4 * Q, PKEYS, K);
-                    const Noise4 n1 = pack_noise(hd, tg + 20 + 4 * Q, PKEYS, K);
-#endif
+                    const Noise4 n0 = pack_noise(hd, tg + 4 * Q, a.k0, a.k1, K);
+                    const Noise4 n1 = pack_noise(hd, tg + 20 + 4 * Q, a.k0, a.k1, K);
                     const float d0[4] = {n0.r0 * n0.c0, n0.r0 * n0.s0, n0.r1 * n0.c1, n0.r1 * n0.s1};
                     const float d1[4] = {n1.r0 * n1.c0, n1.r0 * n1.s0, n1.r1 * n1.c1, n1.r1 * n1.s1};
                     static_for<0, 4>([&](auto ic) {
                         constexpr int i = decltype(ic)::value;
                         x[16 * Q + 4 * g + i] = (i & 1) ? make_float2(-d0[i], -d1[i]) : make_float2(d0[i], d1[i]);
                     });
-#ifndef OFDM_PACK_GEN_SPLIT
-#define OFDM_PACK_GEN_SPLIT 2
-#endif
-                    if constexpr (Q % OFDM_PACK_GEN_SPLIT == OFDM_PACK_GEN_SPLIT - 1 && Q < 3) sched_fence();
+                    if constexpr (Q % PACK_GEN_SPLIT == PACK_GEN_SPLIT - 1 && Q < 3) sched_fence();
                 });
-#ifndef OFDM_ABL_NO_DFFT
                 static_for<0, 4>([&](auto ic) { dif_stage1<false, 4 * g + decltype(ic)::value>(x); });
-#endif
                 sched_fence();
             });
             // ---- bin pairs: noise split, clean spectra, estimate, equaliser, demap of both data symbols
@@ -701,8 +455,8 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
             uint32_t em = 0u, be = 0u, ax = 0u, t0 = 0u, t1 = 0u;
             // LDS operands of a bin pair (both clean spectra and, LS, the E spectrum), loaded PF pairs ahead of
             // their use so that the read latency is covered by the pairs in between (the fences every
-            // OFDM_PACK_FENCE_PAIRS pairs keep the loads where they are written)
-            constexpr int PF = KIND == 2 && !FADE ? OFDM_PACK_PF : 0;
+            // PACK_FENCE_PAIRS pairs keep the loads where they are written)
+            constexpr int PF = KIND == 2 && !FADE ? PACK_PF : 0;
             f4v pc0[PF + 1], pc1[PF + 1];
             float4 pe4[PF + 1];
             auto load_pair = [&](auto pc) {
@@ -742,22 +496,8 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
                 const float2 y1m = make_float2(fmaf(0.5f, B.y, c1.z), fmaf(0.5f, B.x, c1.w));
                 float2 u0k, u0m, u1k, u1m;
                 float rk = 0.f, rm = 0.f;
-#ifdef OFDM_ABL_NO_EQ
-                if constexpr (true) {
-                    const float4 e4 = pe4[slot];
-                    evm += (y0k.x + y0m.y) + (y1k.x + y1m.y) + e4.x;
-                    if constexpr (p < EE_LDS_FIRST) evm += ee[p].x;
-                    (void)t0; (void)t1; (void)sm; (void)u0k; (void)u0m; (void)u1k; (void)u1m; (void)rk; (void)rm;
-                } else
-#endif
                 if constexpr (KIND == 2) {
-                    float ex, ey;
-                    if constexpr (p < EE_LDS_FIRST) {
-                        ex = ee[p].x; ey = ee[p].y;
-                    } else {
-                        const f2v v = eew[(p - EE_LDS_FIRST) * 64];
-                        ex = v.x; ey = v.y;
-                    }
+                    const float ex = ee[p].x, ey = ee[p].y;
                     const float4 e4 = pe4[slot];
                     const float2 Sk = make_float2(fmaf(0.5f, ex, e4.x), fmaf(0.5f, ey, e4.y));
                     const float2 Sm = make_float2(fmaf(0.5f, ex, e4.z), fmaf(-0.5f, ey, e4.w));
@@ -772,12 +512,10 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
                     constexpr float cs = (CONV == OFDM_CONV_C && (k & 1)) ? -1.0f : 1.0f;   // k, k2 same parity
                     u0k = cscale(y0k, cs); u0m = cscale(y0m, cs); u1k = cscale(y1k, cs); u1m = cscale(y1m, cs);
                 }
-#ifndef OFDM_ABL_NO_EQ
                 demap_bin<KIND, DUMP>(u0k, rk, t0, sm, evm, em, data_index(k), deq0, db0);
                 demap_bin<KIND, DUMP>(u0m, rm, t0, sm, evm, em, data_index(k2), deq0, db0);
                 demap_bin<KIND, DUMP>(u1k, rk, t1, sm, evm, em, data_index(k), deq1, db1);
                 demap_bin<KIND, DUMP>(u1m, rm, t1, sm, evm, em, data_index(k2), deq1, db1);
-#endif
                 if constexpr ((p & 3) == 3) {
                     // 16 decisions: im errors at even bit positions, re errors at odd
                     ax += __popc(em);
@@ -787,52 +525,32 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
                 // pin the per-bin EVM terms here: left alone, LLVM sinks the whole fma chain to its
                 // single use after the last pair and keeps every bin's u' alive until then
                 opaque(evm);
-#ifndef OFDM_PACK_FENCE_PAIRS
-#define OFDM_PACK_FENCE_PAIRS 2
-#endif
-                if constexpr (p % OFDM_PACK_FENCE_PAIRS == OFDM_PACK_FENCE_PAIRS - 1) sched_fence();
+                if constexpr (p % PACK_FENCE_PAIRS == PACK_FENCE_PAIRS - 1) sched_fence();
             };
-#ifdef OFDM_ABL_NO_DFFT
-#define PK_SUB16(R) do { } while (0)
-#else
-#define PK_SUB16(R) dif_sub16<false, R>(x)
-#endif
-            PK_SUB16(0);
+            dif_sub16<false, 0>(x);
             static_for<0, 6>(pair);
             sched_fence();
-            PK_SUB16(2);
+            dif_sub16<false, 2>(x);
             static_for<6, 13>(pair);
             sched_fence();
-            PK_SUB16(1);
-            PK_SUB16(3);
+            dif_sub16<false, 1>(x);
+            dif_sub16<false, 3>(x);
             static_for<13, 24>(pair);
-#undef PK_SUB16
             if constexpr (DUMP) {
                 if (dbit0) {
                     dbit0[0] = db0[0]; dbit0[1] = db0[1]; dbit0[2] = db0[2];
                     dbit1[0] = db1[0]; dbit1[1] = db1[1]; dbit1[2] = db1[2];
                 }
             }
-#ifdef OFDM_ABL_NO_CNT
-            if constexpr (true) {
-                asm volatile("" :: "v"(evm), "v"(be), "v"(ax), "v"(valid ? 1 : 0));
-            } else
-#endif
-            if constexpr (WFLUSH) {
-                flush_wave(KIND == 2 ? 4.0f * evm : evm, be, ax, valid, lane, sacc[q]);
-            } else {
-                FrameAcc acc;
-                frame_metrics(acc, KIND == 2 ? 4.0f * evm : evm, be, ax);
-                flush_lanes(acc, valid, slots(q, SPLIT ? lane_fresh() : lane));
-            }
-            }   // !SPLIT
+            FrameAcc acc;
+            frame_metrics(acc, KIND == 2 ? 4.0f * evm : evm, be, ax);
+            flush_lanes(acc, valid, slots(q, lane));
         }
         PK_STAMP(4);                                     // SNR loop
     }
     if constexpr (SUBN > 1) {       // fold the copies into sacc
         __syncthreads();
-        const int ft = SPLIT ? (wv << 6) + lane_fresh() : tid;
-        for (int i = ft; i < min(a.n_snr, SACC_XQ) * 5; i += 256) {
+        for (int i = tid; i < min(a.n_snr, SACC_XQ) * 5; i += 256) {
             const int q = i / 5, k = i % 5;
             unsigned long long v = sacc[q][k];
 #pragma unroll
@@ -840,7 +558,7 @@ __global__ __launch_bounds__(256, KIND == 2 ? (CHAN == OFDM_CHAN_RAYLEIGH4 ? OFD
             sacc[q][k] = v;
         }
     }
-    block_flush(a, sacc, SPLIT ? (wv << 6) + lane_fresh() : tid);
+    block_flush(a, sacc, tid);
     PK_STAMP(5);                                           // block flush
 #ifdef OFDM_PACK_STAMPS
     if (lane == 0)
@@ -896,16 +614,9 @@ int rx_pack_ideal_grid(int64_t n_frames, int device) { return pack_grid<ideal_ke
 // Real-noise sweeps: AWGN with either estimator, and the 4-tap Rayleigh channel with the LS estimator
 // (the ideal-CSI Rayleigh ZF and every complex-noise sweep run the {E, D0, D1} / ideal receivers).
 bool rx_pack_applies(const ofdm_cfg &cfg) {
-#ifdef OFDM_RX_NO_PACK
-    (void)cfg;
-    return false;
-#else
     if (cfg.noise != OFDM_NOISE_REAL) return false;
-#ifndef OFDM_RX_NO_PACK_FADE
     if (cfg.channel == OFDM_CHAN_RAYLEIGH4) return cfg.est == OFDM_EST_LS;
-#endif
     return cfg.channel == OFDM_CHAN_AWGN;
-#endif
 }
 
 void launch_rx_pack(hipStream_t st, const RxArgs &a, const ofdm_cfg &cfg, bool dump, unsigned grid) {

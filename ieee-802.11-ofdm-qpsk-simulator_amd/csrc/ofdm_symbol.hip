@@ -4,7 +4,7 @@
 // sweeps (c2/c3/c4, the benchmark) run the packed receivers of ofdm_rxpack.hip instead (launch_rx);
 // the kernels here serve complex noise, the 4-tap Rayleigh channel (c5) and noiseless runs.
 //
-// K1 (the standalone fft()/ifft()) runs one transform per lane quad (fft64_quad_kernel); the Tx and
+// K1 (the standalone fft()/ifft()) runs one transform per lane quad, staged through LDS (fft64_lds_kernel); the Tx and
 // receiver kernels below keep the register mapping:
 // ONE LANE OWNS ONE 64-SAMPLE WINDOW (a data symbol or the LTF pair); its 64-point FFT
 // lives in that lane's VGPRs (ofdm_device.h).  In LS mode a wave carries 21 frames as lanes
@@ -20,277 +20,38 @@
 #include "ofdm_internal.h"
 #include "ofdm_rxcommon.h"
 
-#ifndef OFDM_RX_LS_WAVES            // waves per SIMD the LS receiver is register-budgeted for
 #define OFDM_RX_LS_WAVES 2      // complex-noise / Rayleigh / noiseless LS: 224 VGPRs, no spill (3: 43-55 spilled, same speed)
-#endif
-#ifndef OFDM_RX_IDEAL_WAVES
 #define OFDM_RX_IDEAL_WAVES 2   // (3: 25-62 spilled)
-#endif
 
 namespace ofdm {
 
-// Diagnostic build (-DOFDM_RX_STAMPS): s_memtime per receiver phase, summed per wave and over the
-// grid.  The stamps' lgkmcnt(0) waits and fences change the schedule: read the phases' SHARES, never
-// this build's run time.  Phases: 0 window + noise + first radix-4 stage, 1 sub-block FFTs,
-// 2 equaliser fetch + demap, 3 frame metrics + counters, 4 group end (wait + barrier).
-#ifdef OFDM_RX_STAMPS
-struct RxStamp {
-    unsigned long long acc[5] = {0, 0, 0, 0, 0};
-    unsigned long long t = 0;
-    __device__ __forceinline__ static unsigned long long now() {
-        unsigned long long v;
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");
-        __builtin_amdgcn_sched_barrier(0);
-        return v;
-    }
-    __device__ __forceinline__ void start() { t = now(); }
-    __device__ __forceinline__ void mark(int k) { const unsigned long long v = now(); acc[k] += v - t; t = v; }
-    __device__ __forceinline__ void flush(unsigned long long *dst) {
-        if (dst && (threadIdx.x & 63) == 0)
-            for (int k = 0; k < 5; ++k) atomicAdd(&dst[k], acc[k]);
-    }
-};
-#else
+// Phase marks of the receivers below (0 window + noise + first radix-4 stage, 1 sub-block FFTs, 2 equaliser
+// fetch + demap, 3 frame metrics + counters, 4 group end).  They compile to nothing; the s_memtime build that
+// measured them (-DOFDM_RX_STAMPS) is in git history (profiles/r06/README.md).
 struct RxStamp {
     __device__ __forceinline__ void start() {}
     __device__ __forceinline__ void mark(int) {}
     __device__ __forceinline__ void flush(unsigned long long *) {}
 };
-#endif
 
 // ======================================================================== K1: batched FFT
-// One wave = 64 transforms.  Coalesced 16-B loads into a padded LDS image (row = 64 float2 + 1
-// pad: conflict-free ds_read_b64 per lane-row), each lane then runs its own register FFT.
-constexpr int K1_ROW = 65;  // float2 per LDS row
-
-template <bool INV, int CONV>
-__global__ __launch_bounds__(64, 2) void fft64_kernel(const float2 *__restrict__ in, float2 *__restrict__ out,
-                                                      int64_t n) {
-    __shared__ float2 lds[64 * K1_ROW];
-    const int lane = threadIdx.x;
-    const int64_t base = (int64_t)blockIdx.x * 64;
-    const int64_t nt = (n - base) < 64 ? (n - base) : 64;   // transforms in this wave
-    const float4 *src = reinterpret_cast<const float4 *>(in + base * 64);
-#pragma unroll 8
-    for (int k = 0; k < 32; ++k) {
-        const int e = k * 128 + lane * 2;   // float2 element index within the wave's block
-        const int row = e >> 6, col = e & 63;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (row < nt) v = src[e >> 1];
-        lds[row * K1_ROW + col] = make_float2(v.x, v.y);
-        lds[row * K1_ROW + col + 1] = make_float2(v.z, v.w);
-    }
-    __syncthreads();
-    float2 x[64];
-    const float2 *row = lds + lane * K1_ROW;
-    static_for<0, 4>([&](auto gc) {
-        constexpr int g = decltype(gc)::value;
-        static_for<0, 16>([&](auto pc) {
-            constexpr int n = 16 * (decltype(pc)::value >> 2) + 4 * g + (decltype(pc)::value & 3);
-            float2 v = row[n];
-            // fft(): DFT of x[n](-1)^n = fftshift(DFT(x)) (OFDM.c:314-318);
-            // ifft(): X~[i] = X[i](-1)^i for the C convention (D5), none for MATLAB
-            if constexpr ((!INV || CONV == OFDM_CONV_C) && (n & 1)) v = make_float2(-v.x, -v.y);
-            x[n] = v;
-        });
-        static_for<0, 4>([&](auto ic) { dif_stage1<INV, 4 * g + decltype(ic)::value>(x); });
-        sched_fence();
-    });
-    __syncthreads();   // every lane has read its row
-    float2 *orow = lds + lane * K1_ROW;
-    static_for<0, 4>([&](auto rc) {
-        constexpr int R = decltype(rc)::value;
-        dif_sub16<INV, R>(x);
-        static_for<0, 16>([&](auto kc) {
-            constexpr int k = 4 * decltype(kc)::value + R;     // bins with k & 3 == R
-            float2 v = x[digit_rev4(k)];
-            if constexpr (INV) v = cscale(v, (k & 1) ? -1.0f / 64.0f : 1.0f / 64.0f);   // (-1)^n / 64
-            orow[k] = v;
-        });
-        sched_fence();
-    });
-    __syncthreads();
-    float4 *dst = reinterpret_cast<float4 *>(out + base * 64);
-#pragma unroll 8
-    for (int k = 0; k < 32; ++k) {
-        const int e = k * 128 + lane * 2;
-        const int r = e >> 6, col = e & 63;
-        if (r < nt) {
-            const float2 a = lds[r * K1_ROW + col], b = lds[r * K1_ROW + col + 1];
-            dst[e >> 1] = make_float4(a.x, a.y, b.x, b.y);
-        }
-    }
-}
-
-// K1 as launched (-DOFDM_K1_LANE selects the kernel above): the north_star's "one FFT per wavefront,
-// radix-4 + __shfl" mapping.  Lane L holds x[L]; each radix-4 DIF stage fetches the four inputs of its
-// butterfly with __shfl (ds_bpermute), forms its own output and applies its twiddle.  K1 is HBM-bound
-// and this mapping streams 3.7-4.2 TB/s against the lane-per-transform kernel's 2.8 TB/s (one wave per
-// SIMD: 174 VGPRs + a 33 KB LDS transpose); it costs ~3.9x the VALU per transform, which is why the
-// VALU-bound receivers keep one window per lane.
-// one radix-4 DIF stage of span 4Q: lane L = base + m Q (+ j) gathers its butterfly's four inputs, forms
-// output m and applies the twiddle w = W_{4Q}^{j m} (precomputed per lane: it does not depend on the
-// transform)
-template <bool INV, int Q>
-__device__ __forceinline__ float2 wave_dif_stage(float2 v, int lane, float2 w) {
-    const int m = (lane / Q) & 3, base = lane - m * Q;
-    float2 a[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int src = base + q * Q;
-        a[q] = make_float2(__shfl(v.x, src, 64), __shfl(v.y, src, 64));
-    }
-    const float2 t0 = cadd(a[0], a[2]), t1 = csub(a[0], a[2]), t2 = cadd(a[1], a[3]), t3 = csub(a[1], a[3]);
-    // y0 = t0 + t2, y2 = t0 - t2, y1 = t1 -/+ j t3, y3 = t1 +/- j t3 (forward / inverse)
-    const float2 jt3 = INV ? make_float2(-t3.y, t3.x) : make_float2(t3.y, -t3.x);
-    const float2 e = (m & 1) ? t1 : t0;
-    const float2 o = (m & 1) ? jt3 : t2;
-    const float2 y = (m == 0 || m == 1) ? cadd(e, o) : csub(e, o);
-    return make_float2(fmaf(y.x, w.x, -y.y * w.y), fmaf(y.x, w.y, y.y * w.x));
-}
-
-template <bool INV, int Q>
-__device__ __forceinline__ float2 wave_twiddle(int lane) {
-    const int m = (lane / Q) & 3, j = lane % Q;
-    float sn, cs;
-    __sincosf((INV ? 6.283185307179586f : -6.283185307179586f) * (float)(j * m) / (float)(4 * Q), &sn, &cs);
-    return make_float2(cs, sn);
-}
-
-#ifndef OFDM_K1_WAVE_T
-#define OFDM_K1_WAVE_T 8    // transforms per wave, their loads issued together (memory-level parallelism)
-#endif
-template <bool INV, int CONV>
-__global__ __launch_bounds__(256) void fft64_wave_kernel(const float2 *__restrict__ in, float2 *__restrict__ out,
-                                                         int64_t n) {
-    constexpr int T = OFDM_K1_WAVE_T;
-    const int lane = threadIdx.x & 63;
-    const int64_t t0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * T;
-    float2 v[T];
-#pragma unroll
-    for (int u = 0; u < T; ++u) v[u] = t0 + u < n ? in[(t0 + u) * 64 + lane] : make_float2(0.f, 0.f);
-    const float2 w16 = wave_twiddle<INV, 16>(lane), w4 = wave_twiddle<INV, 4>(lane);
-    const int k = digit_rev4(lane);                          // lane L ends with bin digit_rev4(L)
-    const float in_sign = ((!INV || CONV == OFDM_CONV_C) && (lane & 1)) ? -1.0f : 1.0f;    // (-1)^n (D5)
-    const float out_scale = INV ? ((k & 1) ? -1.0f / 64.0f : 1.0f / 64.0f) : 1.0f;
-#pragma unroll
-    for (int u = 0; u < T; ++u) {
-        float2 x = cscale(v[u], in_sign);
-        x = wave_dif_stage<INV, 16>(x, lane, w16);
-        x = wave_dif_stage<INV, 4>(x, lane, w4);
-        x = wave_dif_stage<INV, 1>(x, lane, make_float2(1.0f, 0.0f));   // span 4: twiddles are 1
-        if (t0 + u < n) out[(t0 + u) * 64 + k] = cscale(x, out_scale);
-    }
-}
-
-// K1 as launched: FOUR LANES (a quad) PER TRANSFORM.  Lane q of the quad loads the 16 contiguous samples
-// x[16q + j] (128 B: eight 16-byte loads), then
+// FOUR LANES (a quad) PER TRANSFORM.  Lane q of the quad holds the 16 samples x[16q + j], then
 //   X[4k + r] = sum_j W16^{jk} ( W64^{jr} sum_q x[16q + j] W4^{qr} )     (radix-4 DIF, first stage across lanes)
 // the inner 4-point DFT over q runs across the quad as two DPP exchanges (quad_perm xor 2, xor 1), lane q
 // ending with output residue r = bitrev2(q); the twiddles W64^{jr} are per-lane constants held in VGPRs;
-// the 16-point DFT over j runs in the lane's registers (dif4<16>).  No LDS, ~29 VALU wave-instructions
-// per transform against the wavefront mapping's 70 + 24 ds_bpermute, so the kernel is HBM-bound.
-#ifndef OFDM_K1_QUAD_T
-#define OFDM_K1_QUAD_T 1    // transforms per quad with their loads in flight together (A/B: 2 -2 %, 4 -5 %)
-#endif
+// the 16-point DFT over j runs in the lane's registers (dif4<16>).  No cross-lane LDS traffic in the
+// transform itself, ~29 VALU wave-instructions per transform, so the kernel is HBM-bound.  Earlier K1 forms
+// (lane per transform, wavefront per transform with __shfl, the quad kernel with direct HBM access) are in
+// git history (profiles/r06/README.md).
 template <int CTRL>
 __device__ __forceinline__ float2 dpp_f2(float2 v) {
     return make_float2(__int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v.x), CTRL, 0xF, 0xF, false)),
                        __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v.y), CTRL, 0xF, 0xF, false)));
 }
-#ifndef OFDM_K1_NT
-#define OFDM_K1_NT 1        // non-temporal HBM stores (K1; A/B round 5, profiles/r05/ab/k1.txt: LDS kernel +1.7 % with
-                            // <= 128 VGPRs; the quad kernel's scattered 8-byte stores fall to 2.0e9 with them)
-#endif
-#ifndef OFDM_K1Q_WPE
-#define OFDM_K1Q_WPE 1      // A/B option: amdgpu_waves_per_eu lower bound of the quad kernel
-#endif
-template <bool INV, int CONV>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OFDM_K1Q_WPE)))
-void fft64_quad_kernel(const float2 *__restrict__ in, float2 *__restrict__ out, int64_t n) {
-    constexpr int T = OFDM_K1_QUAD_T;
-    const int q = threadIdx.x & 3;
-    const int r = ((q & 1) << 1) | (q >> 1);                      // output residue of this lane
-    const int64_t t0 = ((int64_t)blockIdx.x * 64 + (threadIdx.x >> 2)) * T;
-    // per-lane constants: stage-1 sign, stage-2 coefficients (own * a + partner * b, a, b in {+-1, +-j}),
-    // twiddles W64^{jr} (forward e^{-j...}, inverse e^{+j...}) selected from the exact constant table
-    const float s1 = q < 2 ? 1.0f : -1.0f;
-    const float jf = INV ? -1.0f : 1.0f;                          // -j (forward) / +j (inverse) = jf * (-j)
-    const float2 ca = q == 3 ? make_float2(0.f, jf) : make_float2(q == 1 ? -1.0f : 1.0f, 0.f);
-    const float2 cb = q == 2 ? make_float2(0.f, -jf) : make_float2(1.0f, 0.f);
-    float2 tw[16];
-    static_for<1, 16>([&](auto jc) {
-        constexpr int j = decltype(jc)::value;
-        auto w = [](auto ec) {
-            constexpr int e = decltype(ec)::value % 64;
-            return make_float2(kCos64[e], INV ? kSin64[e] : -kSin64[e]);
-        };
-        const float2 w1 = w(std::integral_constant<int, j>{}), w2 = w(std::integral_constant<int, 2 * j>{}),
-                     w3 = w(std::integral_constant<int, 3 * j>{});
-        tw[j] = r == 1 ? w1 : r == 2 ? w2 : w3;                  // r == 0 lanes: j's twiddle is 1, see below
-        if (r == 0) tw[j] = make_float2(1.0f, 0.0f);
-    });
-    const float out_scale = INV ? ((r & 1) ? -1.0f / 64.0f : 1.0f / 64.0f) : 1.0f;   // bin parity = r parity
-    float2 x[T][64];                                              // x[u][j], j < 16 used
-#pragma unroll
-    for (int u = 0; u < T; ++u) {
-        const int64_t t = t0 + u;
-        const float4 *src = reinterpret_cast<const float4 *>(in + (t < n ? t : 0) * 64 + 16 * q);
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-#ifdef OFDM_K1_ABL_LOAD   // ablation (wrong results): each quad's loads contiguous 64 B per instruction
-            const float4 v = t < n ? src[4 * c - 7 * q] : make_float4(0.f, 0.f, 0.f, 0.f);
-#else
-            const float4 v = t < n ? src[c] : make_float4(0.f, 0.f, 0.f, 0.f);
-#endif
-            x[u][2 * c] = make_float2(v.x, v.y);
-            x[u][2 * c + 1] = make_float2(v.z, v.w);
-        }
-    }
-#pragma unroll
-    for (int u = 0; u < T; ++u) {
-        const int64_t t = t0 + u;
-        static_for<0, 16>([&](auto jc) {
-            constexpr int j = decltype(jc)::value;
-            // (-1)^n input modulation (n = 16q + j: the parity of j), D5
-            constexpr float sg = ((!INV || CONV == OFDM_CONV_C) && (j & 1)) ? -1.0f : 1.0f;
-            float2 v = make_float2(sg * x[u][j].x, sg * x[u][j].y);
-            const float2 p2 = dpp_f2<DPP_QUAD_XOR2>(v);           // stage 1: t = s1 own + partner
-            v = make_float2(fmaf(s1, v.x, p2.x), fmaf(s1, v.y, p2.y));
-            const float2 p1 = dpp_f2<DPP_QUAD_XOR1>(v);           // stage 2: a own + b partner
-            v = make_float2(ca.x * v.x - ca.y * v.y + (cb.x * p1.x - cb.y * p1.y),
-                            ca.x * v.y + ca.y * v.x + (cb.x * p1.y + cb.y * p1.x));
-            if constexpr (j > 0) v = make_float2(fmaf(v.x, tw[j].x, -v.y * tw[j].y), fmaf(v.x, tw[j].y, v.y * tw[j].x));
-            x[u][j] = v;
-        });
-        dif4<INV, 16, 0>(x[u]);                                   // bin k' at position rev16(k')
-        if (t < n) {
-            float2 *dst = out + t * 64 + r;
-            static_for<0, 16>([&](auto pc) {
-                constexpr int pos = decltype(pc)::value;
-                constexpr int kp = ((pos & 3) << 2) | (pos >> 2);   // rev16 is its own inverse
-#ifdef OFDM_K1_ABL_STORE  // ablation (wrong results): every store instruction writes 512 contiguous bytes
-                out[(t0 - (threadIdx.x >> 2) + 16 * (threadIdx.x >> 6)) * 64 + 64 * pos + (threadIdx.x & 63)] = cscale(x[u][pos], out_scale);
-#else
-#if OFDM_K1_NT
-                {
-                    const float2 v = cscale(x[u][pos], out_scale);
-                    __builtin_nontemporal_store(f2v{v.x, v.y}, reinterpret_cast<f2v *>(dst + 4 * kp));
-                }
-#else
-                dst[4 * kp] = cscale(x[u][pos], out_scale);
-#endif
-#endif
-            });
-        }
-    }
-}
-
-// K1 as launched by default: the quad mapping above with BOTH HBM sides coalesced through LDS (round 5;
-// VERDICT r4 item 6).  fft64_quad_kernel's lane q loads 16 B at byte 128 q + 16 c of its transform per
-// instruction, so one wave-instruction touches 64 different 128-B lines (and its stores 16 lines in 32-B pieces);
-// round 2's ablation priced perfectly coalesced loads at +9 % for fft (profiles/r02/k1q/fft_ab.txt).  Here a wave
+// Both HBM sides are coalesced through LDS (round 5): loading each quad lane's 16 B at byte
+// 128 q + 16 c of its transform directly would make one wave-instruction touch 64 different 128-B lines (and its
+// stores 16 lines in 32-B pieces); round 2's ablation priced perfectly coalesced loads at +9 % for fft
+// (profiles/r02/k1q/fft_ab.txt).  Non-temporal stores: +1.7 % (profiles/r05/ab/k1.txt).  A wave
 // owns TPW = 8 transforms (4 KB, contiguous in HBM), quads 0..7 (lanes 0..31) transforming them:
 //   * loads: TPW / 2 LDS-DMA instructions (global_load_lds_dwordx4), each reading 1 KB of HBM contiguously; the lane ->
 //     chunk assignment inside each KB is permuted so that chunk j of transform t lands at slot 32 t + (j ^ s),
@@ -309,16 +70,10 @@ void fft64_quad_kernel(const float2 *__restrict__ in, float2 *__restrict__ out, 
 // 8 (4 KB) 5.82-5.84e9 (+7 %), 4 (2 KB, 3/4 of the lanes idle) 4.17e9.  The same shapes as plain copies
 // (tools/ubench_copy.hip, profiles/r05/ab/copy_ceiling.txt): 8 KB per wave, loaded whole and then stored, 5.5-5.8 TB/s
 // whether staged through LDS or registers and at any occupancy; 4 KB 6.05; 2 KB 6.23; 1 KB 6.27-6.37 TB/s.
-#ifndef OFDM_K1_WPE
 #define OFDM_K1_WPE 4       // amdgpu_waves_per_eu lower bound: <= 128 VGPRs (87: 5 waves/SIMD; 6 spill 6 VGPRs)
-#endif
-#ifndef OFDM_K1_TPW
 #define OFDM_K1_TPW 8       // transforms per wave (16: every quad of the wave; 8 / 4: quads 0..TPW-1 only)
-#endif
 static_assert(OFDM_K1_TPW == 16 || OFDM_K1_TPW == 8 || OFDM_K1_TPW == 4, "whole 1-KB load / store instructions");
-#ifndef OFDM_K1_LOAD_CPOL
 #define OFDM_K1_LOAD_CPOL 2 // cache-policy bits of the LDS-DMA loads: nt (streamed once; A/B +1.5 % on top of the above)
-#endif
 template <bool INV, int CONV>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OFDM_K1_WPE)))
 void fft64_lds_kernel(const float2 *__restrict__ in, float2 *__restrict__ out, int64_t n) {
@@ -409,11 +164,7 @@ void fft64_lds_kernel(const float2 *__restrict__ in, float2 *__restrict__ out, i
         typedef const __attribute__((address_space(3))) f4v lf4c;
         const f4v v = *(lf4c *)(wb + 32 * tg + (m ^ (2 * (tg & 3))));
         if (g < avail) {
-#if OFDM_K1_NT
             __builtin_nontemporal_store(v, reinterpret_cast<f4v *>(dst) + g);
-#else
-            dst[g] = make_float4(v.x, v.y, v.z, v.w);
-#endif
         }
     }
 }
@@ -533,37 +284,17 @@ __device__ __forceinline__ void rx_load(float2 (&c)[7], const WS &src) {
 // K = noise_k(sigma) (real) or noise_k(sigma / sqrt2) (complex): each noisy component is one fma.
 // `hd` = philox_head of the frame's noise stream at this SNR point; `tb` = the counter word c2 of
 // the window's first Philox block (t0 / 4 real, t0 / 2 complex).
-// Ablation builds (diagnostics only, results are wrong): OFDM_ABL_NO_PHILOX replaces the Philox
-// rounds by one multiply, OFDM_ABL_NO_BM drops the Box-Muller transcendentals, OFDM_ABL_NO_BPERM
-// equalises with the lane's own bins, OFDM_ABL_NO_DEMAP folds the bins into one sum.  Their run time
-// against the real kernel prices each stage including its stalls.
+// (The ablation builds that priced each stage, OFDM_ABL_*, are in git history: profiles/r06/README.md.)
 // Philox outputs of one group (samples 4g..4g+3 of each quarter): real noise 4 blocks (c2 = tb + g +
 // 4i), complex 8 (c2 = tb + 2g + 8i + {0, 1}), computed together with VGPR round keys.
 template <int NB>
 __device__ __forceinline__ void rx_philox(const PhiloxHead &hd, const uint32_t (&c2)[NB], uint32_t k0, uint32_t k1,
                                           uint4 (&o)[NB]) {
-#ifdef OFDM_ABL_NO_PHILOX
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-        const uint64_t p = (uint64_t)PHILOX_M1 * (c2[b] ^ hd.n2);
-        o[b] = make_uint4((uint32_t)p, (uint32_t)(p >> 32), (uint32_t)p ^ hd.c3, (uint32_t)(p >> 32) ^ k0);
-    }
-#elif defined(OFDM_RX_VGPR_KEYS)
-    philox10_c2_vk<NB>(hd, c2, k0, k1, o);      // A/B: c3 -1.9 % (register pressure)
-#else
 #pragma unroll
     for (int b = 0; b < NB; ++b) o[b] = philox10_c2(hd, c2[b], k0, k1);
-#endif
 }
 __device__ __forceinline__ Noise4 rx_noise4(uint4 o, float K) {
-#ifdef OFDM_ABL_NO_BM
-    Noise4 n;
-    n.r0 = K * (float)o.x; n.r1 = K * (float)o.z;
-    n.c0 = (float)o.y; n.s0 = n.c0 * 0.5f; n.c1 = (float)o.w; n.s1 = n.c1 * 0.5f;
-    return n;
-#else
     return noise4_of(o, K);
-#endif
 }
 
 // o: the block(s) of samples n0..n0+3 (one for real noise, two for complex)
@@ -599,8 +330,8 @@ __device__ __forceinline__ void rx_noisy(float2 (&x)[64], const float2 (&c)[7], 
 }
 
 // generate the window fused with the first radix-4 stage (4 butterflies per group of 16 samples).
-// OFDM_RX_EARLY_LOADS pins the group's LDS reads ahead of its noise generation; measured slower
-// (+32 live VGPRs -> more spills; the read latency is already hidden by the other 2 waves/SIMD).
+// Pinning the group's LDS reads ahead of its noise generation measured slower (+32 live VGPRs -> more
+// spills; the read latency is already hidden by the other 2 waves/SIMD).
 template <int NOISE, int CHAN, typename WS>
 __device__ __forceinline__ void rx_window_stage1(float2 (&x)[64], const WS &src, uint32_t f_lo,
                                                  uint32_t f_hi, uint32_t t0, uint32_t q, float sigma,
@@ -625,14 +356,12 @@ __device__ __forceinline__ void rx_window_stage1(float2 (&x)[64], const WS &src,
             rx_philox<NB>(hd, c2, k0, k1, o);
         }
     };
-#ifndef OFDM_RX_NO_PIPE_PHILOX
     // software pipeline: group g + 1's Philox chains share group g's fence region with its Box-Muller,
     // noise and butterflies (the next group's 16 state VGPRs fit while x is still partly empty).
     // A/B (profiles/r02/ab): c3 -2.0 %, c2 -4.9 % receiver time
     uint4 on[NB];
     philox_group(std::integral_constant<int, 0>{}, on);
     sched_fence();
-#endif
     static_for<0, 4>([&](auto gc) {
         constexpr int g = decltype(gc)::value;
         float2 c[4][7];
@@ -640,17 +369,10 @@ __device__ __forceinline__ void rx_window_stage1(float2 (&x)[64], const WS &src,
         rx_load<CHAN, 16 + 4 * g>(c[1], src);
         rx_load<CHAN, 32 + 4 * g>(c[2], src);
         rx_load<CHAN, 48 + 4 * g>(c[3], src);
-#ifdef OFDM_RX_EARLY_LOADS
-        sched_fence();
-#endif
         uint4 o[NB];
-#ifndef OFDM_RX_NO_PIPE_PHILOX
 #pragma unroll
         for (int b = 0; b < NB; ++b) o[b] = on[b];
         if constexpr (g < 3) philox_group(std::integral_constant<int, g + 1>{}, on);
-#else
-        philox_group(gc, o);
-#endif
         rx_noisy<NOISE, CHAN, 4 * g>(x, c[0], o + 0 * PB, K, h);
         rx_noisy<NOISE, CHAN, 16 + 4 * g>(x, c[1], o + 1 * PB, K, h);
         rx_noisy<NOISE, CHAN, 32 + 4 * g>(x, c[2], o + 2 * PB, K, h);
@@ -669,39 +391,15 @@ __device__ __forceinline__ void finish_symbol(float2 (&x)[64], const TW &truth, 
                                               unsigned long long *slots, RxStamp &sp) {
     SymState st;
     sym_init(st);
-#ifdef OFDM_RX_PIPE_FFT
-    // software pipeline: sub-block R + 1's FFT (in place, no extra registers) and its equaliser fetch
-    // share sub-block R's demap region.  A/B: c3 +1.2 % receiver time (not adopted)
-    dif_sub16<false, 0>(x);
-    Hof.template prefetch<0>(x);
-    sched_fence();
-    static_for<0, 4>([&](auto rc) {
-        constexpr int R = decltype(rc)::value;
-        demap_sub<DUMP, R, KIND>(x, truth.template word<R>(), Hof, dump_eq, st);
-        if constexpr (R < 3) {
-            dif_sub16<false, R + 1>(x);
-            Hof.template prefetch<R + 1>(x);
-        }
-        sched_fence();
-    });
-#else
     static_for<0, 4>([&](auto rc) {
         constexpr int R = decltype(rc)::value;
         dif_sub16<false, R>(x);
         sp.mark(1);
-#ifdef OFDM_ABL_NO_DEMAP
-        static_for<0, 16>([&](auto kc) {
-            constexpr int bin = 4 * decltype(kc)::value + R;
-            if constexpr (data_index(bin) >= 0) st.evm_pre += x[digit_rev4(bin)].x + x[digit_rev4(bin)].y;
-        });
-#else
         Hof.template prefetch<R>(x);
         demap_sub<DUMP, R, KIND>(x, truth.template word<R>(), Hof, dump_eq, st);
-#endif
         sched_fence();
         sp.mark(2);
     });
-#endif
     if constexpr (DUMP) {
         if (dump_bits) { dump_bits[0] = st.d[0]; dump_bits[1] = st.d[1]; dump_bits[2] = st.d[2]; }
     }
@@ -761,18 +459,11 @@ struct LsBpermuteEq {
             constexpr int bin = 4 * decltype(kc)::value + R;
             if constexpr (data_index(bin) >= 0) {
                 const float2 Y = x[digit_rev4(bin)];
-#ifdef OFDM_ABL_NO_BPERM
-                S[decltype(kc)::value] = Y;
-                if (false)
-#endif
                 S[decltype(kc)::value] = make_float2(
                     __int_as_float(__builtin_amdgcn_ds_bpermute((int)e_addr, __float_as_int(Y.x))),
                     __int_as_float(__builtin_amdgcn_ds_bpermute((int)e_addr, __float_as_int(Y.y))));
             }
         });
-#ifdef OFDM_RX_BATCH_BPERM
-        sched_fence();   // issue the sub-block's 24 crossbar reads as one batch, ahead of their uses
-#endif
     }
     template <typename B>
     __device__ __forceinline__ EqOut<2> operator()(float2 Y, B) const {
@@ -824,16 +515,10 @@ __global__ __launch_bounds__(256, OFDM_RX_LS_WAVES) void rx_ls_kernel(RxArgs a) 
         stage_group<G>(a, grp * LS_GROUP_SYMS, sbuf[0], a.ltf2_rows, wv, lane);
         stage_truth(a, grp * LS_GROUP_SYMS, &struth[0][0][0], wv, lane, LS_GROUP_SYMS);
     }
-#ifndef OFDM_RX_STATIC_GROUPS
     if (threadIdx.x == 0) next_group[1] = (int)gridDim.x + (int)atomicAdd(a.work, 1ull);
-#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-#ifndef OFDM_RX_STATIC_GROUPS
     int64_t nxt = __builtin_amdgcn_readfirstlane(next_group[1]);
-#else
-    int64_t nxt = grp + gridDim.x;
-#endif
     RxStamp sp;
     sp.start();
     for (; grp < n_groups;) {
@@ -842,10 +527,8 @@ __global__ __launch_bounds__(256, OFDM_RX_LS_WAVES) void rx_ls_kernel(RxArgs a) 
         const uint64_t f = a.first_frame + (uint64_t)fl;
         const uint32_t f_lo = (uint32_t)f, f_hi = (uint32_t)(f >> 32);
         float2 h[4] = {make_float2(1.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f)};
-#ifndef OFDM_RX_STATIC_GROUPS
         // the group after nxt (read after this group's closing barrier; the previous value was read before it)
         if (threadIdx.x == 0) next_group[par] = (int)gridDim.x + (int)atomicAdd(a.work, 1ull);
-#endif
         if constexpr (FADE) {
             // lane = staged column: 0..41 the data symbols (in place), 42..62 frame lane - 42's 2T (x) h
             const bool dcol = lane < LS_GROUP_SYMS;
@@ -900,11 +583,7 @@ __global__ __launch_bounds__(256, OFDM_RX_LS_WAVES) void rx_ls_kernel(RxArgs a) 
         sp.mark(4);
         cur ^= 1;
         grp = nxt;
-#ifndef OFDM_RX_STATIC_GROUPS
         nxt = __builtin_amdgcn_readfirstlane(next_group[par]);
-#else
-        nxt = grp + gridDim.x;
-#endif
         par ^= 1;
     }
     sp.flush(a.stamps);
@@ -997,36 +676,16 @@ __global__ __launch_bounds__(256, OFDM_RX_IDEAL_WAVES) void rx_ideal_kernel(RxAr
 }
 
 // ======================================================================== launchers
-#ifndef OFDM_K1_LDS
-#define OFDM_K1_LDS 1       // K1 through LDS with coalesced HBM loads and stores (fft64_lds_kernel); 0: fft64_quad_kernel
-#endif
 template <bool INV>
-static void launch_fft_conv(int conv, dim3 g, hipStream_t st, const float2 *in, float2 *out, int64_t n) {
-#if OFDM_K1_LDS && !defined(OFDM_K1_LANE) && !defined(OFDM_K1_WAVE)
+static void launch_fft_conv(int conv, hipStream_t st, const float2 *in, float2 *out, int64_t n) {
     const dim3 gl((unsigned)((n + 4 * OFDM_K1_TPW - 1) / (4 * OFDM_K1_TPW)));
     if (conv == OFDM_CONV_C) hipLaunchKernelGGL((fft64_lds_kernel<INV, OFDM_CONV_C>), gl, dim3(256), 0, st, in, out, n);
     else hipLaunchKernelGGL((fft64_lds_kernel<INV, OFDM_CONV_MATLAB>), gl, dim3(256), 0, st, in, out, n);
-    (void)g;
-#elif !defined(OFDM_K1_LANE) && !defined(OFDM_K1_WAVE)
-    const dim3 gq((unsigned)((n + 64 * OFDM_K1_QUAD_T - 1) / (64 * OFDM_K1_QUAD_T)));
-    if (conv == OFDM_CONV_C) hipLaunchKernelGGL((fft64_quad_kernel<INV, OFDM_CONV_C>), gq, dim3(256), 0, st, in, out, n);
-    else hipLaunchKernelGGL((fft64_quad_kernel<INV, OFDM_CONV_MATLAB>), gq, dim3(256), 0, st, in, out, n);
-    (void)g;
-#elif !defined(OFDM_K1_LANE)    // A/B: one transform per wavefront
-    const dim3 gw((unsigned)((n + 4 * OFDM_K1_WAVE_T - 1) / (4 * OFDM_K1_WAVE_T)));
-    if (conv == OFDM_CONV_C) hipLaunchKernelGGL((fft64_wave_kernel<INV, OFDM_CONV_C>), gw, dim3(256), 0, st, in, out, n);
-    else hipLaunchKernelGGL((fft64_wave_kernel<INV, OFDM_CONV_MATLAB>), gw, dim3(256), 0, st, in, out, n);
-    (void)g;
-#else
-    if (conv == OFDM_CONV_C) hipLaunchKernelGGL((fft64_kernel<INV, OFDM_CONV_C>), g, dim3(64), 0, st, in, out, n);
-    else hipLaunchKernelGGL((fft64_kernel<INV, OFDM_CONV_MATLAB>), g, dim3(64), 0, st, in, out, n);
-#endif
 }
 
 void launch_fft64(hipStream_t st, const float2 *in, float2 *out, int64_t n, int inverse, int conv) {
-    const dim3 g((unsigned)((n + 63) / 64));
-    if (inverse) launch_fft_conv<true>(conv, g, st, in, out, n);
-    else launch_fft_conv<false>(OFDM_CONV_C, g, st, in, out, n);
+    if (inverse) launch_fft_conv<true>(conv, st, in, out, n);
+    else launch_fft_conv<false>(OFDM_CONV_C, st, in, out, n);
 }
 
 void launch_tx(hipStream_t st, const TxArgs &a, int conv) {
@@ -1086,12 +745,6 @@ int rx_grid(const ofdm_cfg &cfg, int64_t n_frames, int device) {
         : reinterpret_cast<const void *>(&rx_ideal_kernel<OFDM_CONV_C, OFDM_NOISE_REAL, OFDM_CHAN_AWGN, false>);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1) cus = 256;
-#ifdef OFDM_RX_GRID_ENV   // diagnostic builds: OFDM_RX_BLOCKS_PER_CU caps the resident blocks per CU
-    if (const char *e = getenv("OFDM_RX_BLOCKS_PER_CU")) {
-        const int v = atoi(e);
-        if (v >= 1 && v < per_cu) per_cu = v;
-    }
-#endif
     const int64_t cap = (int64_t)per_cu * cus;
     const int64_t g = need < cap ? need : cap;
     return (int)(g < 1 ? 1 : g);

@@ -1,6 +1,9 @@
 """LDS bank-conflict attribution of frame_sync_kernel from tools/lds_attrib.sh's PMC passes.
 
-usage: python tools/lds_attrib.py gpurun_out/lds_attrib [--items N] [--out profiles/r05/lds_attrib.json]
+usage: python tools/lds_attrib.py gpurun_out/lds_attrib [--items N] [--out profiles/r05/lds/lds_attrib.json]
+
+The FRAME_DUP_<SITE> probes were pruned from csrc/ in round 6 (profiles/r06/README.md): build the variant libraries
+from a checkout of commit aec0f2e (`git worktree add /tmp/probe aec0f2e`, then tools/build_variants.py there).
 
 Each FRAME_DUP_<SITE> variant issues one access site's LDS instructions twice (same instruction form and lane
 addresses, the duplicate waited for at once; ofdm_frame.hip dup_*), so its SQ_INSTS_LDS / SQ_LDS_BANK_CONFLICT /

@@ -2,6 +2,7 @@
 # LDS conflict attribution of frame_sync_kernel: one PMC pass (SQ_INSTS_LDS, SQ_LDS_BANK_CONFLICT, SQ_LDS_IDX_ACTIVE,
 # SQ_WAVES) of the frame bench per variant library (default + the FRAME_DUP_<SITE> probes, tools/build_variants.py);
 # tools/lds_attrib.py turns the deltas into per-site instruction / conflict / array-cycle counts per item.
+# The probes were pruned from csrc/ in round 6: their libraries are built from commit aec0f2e (profiles/r06/README.md).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp PYTHONDONTWRITEBYTECODE=1

@@ -8,6 +8,9 @@ plus what the ablation leaves in its place (counted below from the replacement c
 tools/isa_mix.py (SIMD cycles per wave-instruction at 2 waves/SIMD).  Whatever no ablation removes (LDS address
 arithmetic, the Hermitian pair untangling of the data noise, loop control) is the remainder row.
 
+The OFDM_ABL_* ablations were pruned from csrc/ in round 6 (profiles/r06/README.md): run this tool in a checkout of
+commit aec0f2e (`git worktree add /tmp/abl aec0f2e`).
+
 Per frame and SNR point the loop draws 48 Philox blocks (16 for the LTF pair, 32 for the data windows) and 96 Box-
 Muller pairs, runs one 32-point (LTF pair) and one 64-point complex (D0 + j D1) FFT, 24 bin pairs of estimate /
 equaliser / slicer / demap for both data symbols, and one frame's counters.
