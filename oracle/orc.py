@@ -9,8 +9,9 @@ from pathlib import Path
 import numpy as np
 
 ORACLE_DIR = Path(__file__).resolve().parent
-ORACLE_SO = ORACLE_DIR / "_lib" / "liboracle.so"
-REF_SO = ORACLE_DIR / "_ref" / "libofdm_ref.so"
+# OFDM_ORACLE_SO / OFDM_REF_SO: other builds of the same sources (tools/sanitize.py's ASan builds in _asan/)
+ORACLE_SO = Path(os.environ.get("OFDM_ORACLE_SO", ORACLE_DIR / "_lib" / "liboracle.so"))
+REF_SO = Path(os.environ.get("OFDM_REF_SO", ORACLE_DIR / "_ref" / "libofdm_ref.so"))
 REF_SRC = Path(os.environ.get("OFDM_REF_SRC", "/root/reference/src/OFDM.c"))
 
 NCOUNTERS = 16
