@@ -124,8 +124,10 @@ __host__ __device__ __forceinline__ uint32_t snr_divmod(uint32_t x, uint32_t d, 
         if (threadIdx.x == 0) stamp_acc[k] += t_ - stamp_t;                          \
         stamp_t = t_;                                                                \
     } while (0)
+constexpr bool FRAME_STAMPS_BUILD = true;   // frame_sync_long_kernel has no stamps: long captures run generic
 #else
 #define FR_STAMP(k) do { } while (0)
+constexpr bool FRAME_STAMPS_BUILD = false;
 #endif
 
 // ======================================================================== K4a: waveform
@@ -1120,9 +1122,10 @@ __global__ __launch_bounds__(64 * W, FRAME_SYNC_MINW) void frame_sync_kernel(Fra
 // LS estimate + CP strip + fft + ZF + slicer + demap (OFDM.c:830-1165) for a batch of items: a quad
 // carries the LTF-sum window in its lane 0 (the estimate, broadcast inside the quad by DPP) and dpq data
 // windows in its last dpq lanes: {LTF, LTF, D_2k, D_2k+1} for 1..2 data symbols and the reference frame's sweep,
-// {LTF, D_3k, D_3k+1, D_3k+2} for 3..8 (ceil(n_data / 3) quads per item instead of ceil(n_data / 2): the 8-symbol
-// message's items take 12 lanes, not 16).  The host picks dpq through the tile size a.ipb = 64 / quads per item
-// (sym_quads), from which the kernel derives it back.
+// {LTF, D_3k, D_3k+1, D_3k+2} for 3 and 5..8 (ceil(n_data / 3) quads per item instead of ceil(n_data / 2): the
+// 8-symbol message's items take 12 lanes, not 16).  The host picks dpq through the tile size a.ipb = 64 / quads per
+// item (sym_quads), from which the kernel derives it back as max(2, ceil(n_data / quads)): for 4 data symbols that
+// is 2 quads of {LTF, LTF, D, D}, the same 8 lanes as {LTF, D, D, D} would take.
 template <bool DUMP, int FIX_ND>   // DUMP: item 0's bits / subcarriers / metrics for ofdm_receiver
 #define FRAME_SYM_MINB 2   // 3 waves/SIMD spills 196 VGPRs: frame mode 9 % slower
 // FIX_ND > 0: n_data as a compile-time constant (the reference message's sweep: the hand-off offsets fold)
@@ -1793,7 +1796,8 @@ static int run_frame_chunk(Ctx *c, FrameArgs &a) {
     // (the equivalence test)
     const bool is_long = a.cap_len > FRAME_LONG_MIN_CAP && a.cap_len - 47 <= 3 * 64 * 31 && !a.ext && !a.dbg_res &&
                          !a.dbg_ints && !a.dbg_bits && !a.dbg_eq && !a.dbg_corr && !a.dbg_frame && !a.word_stats &&
-                         2 * fr_len(a.n_data) + 40 <= FRAME_LONG_REGION && !getenv("OFDM_FRAME_NO_LONG");
+                         2 * fr_len(a.n_data) + 40 <= FRAME_LONG_REGION && !getenv("OFDM_FRAME_NO_LONG") &&
+                         !FRAME_STAMPS_BUILD;
     if (is_long) {
         a.region_floats = FRAME_LONG_REGION;
         const size_t lds_l = (size_t)a.n_snr * 2 * 8 + (((size_t)a.imt_len * 4 + 15) & ~size_t(15)) +

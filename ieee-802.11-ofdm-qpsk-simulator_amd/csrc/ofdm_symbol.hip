@@ -76,12 +76,13 @@ static_assert(OFDM_K1_TPW == 16 || OFDM_K1_TPW == 8 || OFDM_K1_TPW == 4, "whole 
 #define OFDM_K1_LOAD_CPOL 2 // cache-policy bits of the LDS-DMA loads: nt (streamed once; A/B +1.5 % on top of the above)
 template <bool INV, int CONV>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OFDM_K1_WPE)))
-void fft64_lds_kernel(const float2 *__restrict__ in, float2 *__restrict__ out, int64_t n) {
+void fft64_lds_kernel(const float2 *in, float2 *out, int64_t n) {   // in == out allowed: not __restrict__
     constexpr int TPW = OFDM_K1_TPW;
     __shared__ __attribute__((aligned(16))) float4 buf[4][32 * TPW];  // per wave: TPW transforms x 32 chunks of 16 B
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t t_base = ((int64_t)blockIdx.x * 4 + wv) * TPW;      // this wave's first transform
-    const int64_t avail = (n - t_base) * 32;                           // chunks of this wave that exist (>= 1)
+    const int64_t avail = (n - t_base) * 32;                           // chunks of this wave that exist (<= 0:
+                                                                       // a trailing wave of the last block)
     float4 *wb = buf[wv];
     const float4 *src = reinterpret_cast<const float4 *>(in) + t_base * 32;
 #pragma unroll

@@ -511,3 +511,21 @@ def test_launch_ranks_relays_one_line(monkeypatch, capsys):
         assert rc == rc_want and out.out.strip() == out_want, script
         if rc_want == 0:
             assert "progress" in out.err
+
+
+def test_pmc_trace_fallback_matches_stats(tmp_path):
+    """ADVICE r5: tools/pmc_summary.read_trace sums the kernel-trace rows where a record has no --stats summary;
+    on a record that has both (round 4's certified c3 PMC run) the two agree exactly."""
+    import shutil
+    sys.path.insert(0, str(ROOT / "tools"))
+    import pmc_summary
+    src = ROOT / "profiles" / "r04" / "pmc" / "c3"
+    a = pmc_summary.read_trace(src)
+    dst = tmp_path / "c3"
+    shutil.copytree(src / "pmc_trace", dst / "pmc_trace")
+    for f in dst.glob("pmc_trace/**/*kernel_stats.csv"):
+        f.unlink()
+    b = pmc_summary.read_trace(dst)
+    assert a and a.keys() == b.keys()
+    for k in a:
+        assert a[k]["calls"] == b[k]["calls"] and a[k]["total_ns"] == pytest.approx(b[k]["total_ns"])

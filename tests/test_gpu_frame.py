@@ -183,9 +183,10 @@ def test_long_capture_kernel_equals_generic(pkg, monkeypatch, msg_len):
     """Frames of >= 5 data symbols (captures > 4,100 samples) run frame_sync_long_kernel: two resident capture
     pieces per wave (the last detection round's samples, then [0, 4,016)), the matched-filter window generated again
     when it leaves the resident piece, fr[] over the region.  Every counter and packet_idx equals the generic
-    kernel's (OFDM_FRAME_NO_LONG=1), over the bench's SNR grid, for 8-, 7- and 5-symbol messages (two rounds of
-    detection for the 5-symbol 4,482-sample captures, three for the others).  Chunked long sweeps (chunk starts off
-    the SNR grid) are test_frame_sweep_nomem_halving_and_nonzero_q0[message8]."""
+    kernel's (OFDM_FRAME_NO_LONG=1), over the bench's SNR grid, for 8-, 7- and 5-symbol messages.  Every long capture
+    has three detection rounds (its Lc > 2 x 1,984 positions); the 5-symbol 4,482-sample capture's last round is only
+    467 positions long.  Chunked long sweeps (chunk starts off the SNR grid) are
+    test_frame_sweep_nomem_halving_and_nonzero_q0[message8]."""
     snrs = np.arange(0.0, 31.0, 2.0)
     msg = (b"The long-capture kernel keeps two pieces of the capture resident per wave. " * 2)[:msg_len]
     with pkg.Engine(0) as e:
@@ -221,12 +222,12 @@ def test_long_capture_lazy_equals_full_evaluation(pkg, monkeypatch):
     assert np.mean(lp[-4:] > 0) > 0.99
 
 
-@pytest.mark.parametrize("msg_len", [96, 49, 30])
+@pytest.mark.parametrize("msg_len", [96, 49, 40, 30])
 def test_symbol_kernel_three_data_lanes_per_quad(pkg, monkeypatch, msg_len):
     """Messages of 3..8 data symbols run frame_sym_kernel with quads {LTF, D, D, D} (ceil(n_data / 3) quads per
     item; 12 lanes per 8-symbol item instead of 16).  Every counter and packet_idx equals the {LTF, LTF, D, D}
-    layout (OFDM_FRAME_SYM_DPQ2=1), for 8-, 5- and 3-symbol messages: the item totals are summed in symbol order
-    either way."""
+    layout (OFDM_FRAME_SYM_DPQ2=1), for 8-, 5-, 4- and 3-symbol messages: the item totals are summed in symbol order
+    either way.  (4 symbols: the kernel derives 2 data lanes per quad from the 2-quad tile)"""
     snrs = np.array([0.0, 6.0, 10.0, 14.0, 20.0, 30.0])
     msg = (b"three data lanes per quad in the symbol kernel, one lane for the LTF estimate. " * 2)[:msg_len]
     with pkg.Engine(0) as e:

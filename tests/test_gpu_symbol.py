@@ -43,6 +43,26 @@ def test_fft64_conventions_and_ragged(engine, oracle):
             assert normwise(im[k], oracle.ifft64(x[k].astype(np.complex128), "matlab")) < 1e-6
 
 
+def test_fft64_in_place_ragged(engine, oracle):
+    """fft64_into(x, x) (in == out, which fft64_lds_kernel allows: a wave reads all its transforms
+    before it writes any) for ragged n, forward and inverse, against the oracle; the rows past n of the
+    underlying buffer are untouched."""
+    import torch
+    rng = np.random.default_rng(11)
+    for n, inverse in ((65, False), (65, True), (7, False), (1000, True)):
+        buf = (rng.standard_normal((n + 40, 64)) + 1j * rng.standard_normal((n + 40, 64))).astype(np.complex64)
+        d = to_dev(buf)
+        x = d[:n]
+        engine.fft64_into(x, x, inverse=inverse, conv="c")
+        torch.cuda.synchronize()
+        got = d.cpu().numpy()
+        for k in (0, n // 2, n - 1):
+            want = (oracle.ifft64(buf[k].astype(np.complex128), "c") if inverse
+                    else oracle.fft64(buf[k].astype(np.complex128)))
+            assert normwise(got[k], want) < 1e-6, (n, inverse, k)
+        assert np.array_equal(got[n:].view(np.uint32), buf[n:].view(np.uint32)), (n, inverse)
+
+
 def test_fft64_roundtrip_large(engine):
     import torch
     n = 1 << 20

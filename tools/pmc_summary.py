@@ -62,16 +62,28 @@ def read_counters(d: Path):
 
 
 def read_trace(d: Path):
+    """Per-kernel calls / total / mean duration of the pmc_trace run: from rocprofv3's --stats summary, or, where
+    a record keeps only the kernel trace, summed from its dispatch rows."""
     out = {}
-    for f in sorted(d.glob("pmc_trace/**/*kernel_stats.csv")):
+
+    def add(name, calls, ns):
+        k = kernel_key(name)
+        if k:       # several instantiations of one kernel (fft64: forward and inverse) are summed
+            e = out.setdefault(k, {"calls": 0, "total_ns": 0.0})
+            e["calls"] += calls
+            e["total_ns"] += ns
+            e["avg_ns"] = e["total_ns"] / e["calls"]
+
+    stats = sorted(d.glob("pmc_trace/**/*kernel_stats.csv"))
+    for f in stats:
         with open(f) as fh:
             for r in csv.DictReader(fh):
-                k = kernel_key(r["Name"])
-                if k:   # several instantiations of one kernel (fft64: forward and inverse) are summed
-                    e = out.setdefault(k, {"calls": 0, "total_ns": 0.0})
-                    e["calls"] += int(r["Calls"])
-                    e["total_ns"] += float(r["TotalDurationNs"])
-                    e["avg_ns"] = e["total_ns"] / e["calls"]
+                add(r["Name"], int(r["Calls"]), float(r["TotalDurationNs"]))
+    if not stats:
+        for f in sorted(d.glob("pmc_trace/**/*kernel_trace.csv")):
+            with open(f) as fh:
+                for r in csv.DictReader(fh):
+                    add(r["Kernel_Name"], 1, float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
     return out
 
 
