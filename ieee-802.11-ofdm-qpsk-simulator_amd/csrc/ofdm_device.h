@@ -367,9 +367,13 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 __device__ __forceinline__ float atan2_cfo(float y, float x) {
     float ax = fabsf(x), ay = fabsf(y);
     const float m = fmaxf(ax, ay);
-    const float sc = m < 0x1p-64f ? 0x1p64f : m > 0x1p64f ? 0x1p-64f : 1.0f;    // exact power-of-two scaling
-    ax *= sc;
-    ay *= sc;
+    // the rescale sits behind a wave-uniform branch: a CFO sum is in range on every lane (it added ~6
+    // VALU per call on the frame path when done unconditionally)
+    if (__builtin_expect(__ballot(!(m >= 0x1p-64f && m <= 0x1p64f)) != 0ull, 0)) {
+        const float sc = m < 0x1p-64f ? 0x1p64f : m > 0x1p64f ? 0x1p-64f : 1.0f;    // exact power-of-two scaling
+        ax *= sc;
+        ay *= sc;
+    }
     const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
     float a = mn * __builtin_amdgcn_rcpf(mx);
     a = mn > 0.f ? a : 0.f;                                        // 0 / 0 and 0 / m: 0

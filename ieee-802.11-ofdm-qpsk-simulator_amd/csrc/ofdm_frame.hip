@@ -379,6 +379,19 @@ constexpr size_t FRAME_LDS_PER_CU = 160 * 1024;
 constexpr int SYNC_WAVES = FRAME_SYNC_WAVES;
 constexpr int SYNC_THREADS = 64 * SYNC_WAVES;
 constexpr int IMT_EXT = 128;         // table slack past one waveform copy: a lane's longest contiguous read
+// The fixed-geometry kernel's layout: FIX_W waves per block sharing FIX_IMT_COPIES consecutive
+// copies of the imaginary-part period.  With one copy every lane reduces its own table index mod the period, and the
+// lanes past the wrap land 12 banks off the others (2-way conflicts on every imaginary detection load); with enough
+// copies a detection round or a matched-filter pass reduces ONE uniform base and its lanes read a linear run (no
+// lane-dependent wrap).  Three copies cover round 0's 2,031 samples from any start; 12-wave blocks (one per CU, the
+// same 3 waves per SIMD) pay the table once per CU: 256 + 12,272 + 12 x 12,080 B = 157.5 KB.  Round 6 A/B
+// (profiles/r06/frame/ab_layouts.txt): LDS conflicts 35.7 -> 23.6 % of the sync kernel's LDS array cycles, frame
+// +1.4 % (5.37 -> 5.45e8); 12-wave blocks with one copy alone +0.0 %, three copies at 4-wave blocks -15 % (two blocks
+// per CU).
+constexpr int FIX_W = 12, FIX_IMT_COPIES = 3;
+// Bank-balanced round-1 chunk starts (DetGeom::r1_start_of): conflicts 23.6 -> 10.5 %, but 15 more VALU per item for
+// the start / owner arithmetic and -0.6 % (profiles/r06/frame/ab_balanced_r1.txt): off
+constexpr bool LDS_BALANCED_R1 = false;
 constexpr int DET_B = 16;           // detection positions per batch (= samples per register block)
 // detection positions per lane and round: the largest odd chunk whose ceil(chunk / DET_B) batches fit one
 // 64-bit crossing mask (63 for DET_B = 16); at most 2 rounds
@@ -398,7 +411,17 @@ static_assert(64 * 2 * DET_MAX_CHUNK + 47 >= CAP_ABS_MAX, "two detection rounds 
 struct DetGeom {
     int c0, c1, x1, B1, R;
     // first position of lane l's round-1 chunk, relative to B1
-    __host__ __device__ int r1_start(int l) const { return l * c1 + ((l * x1) >> 6); }
+    __host__ __device__ int r1_start(int l) const { return r1_start_of(c1, x1, l); }
+    // x1 of the 64 chunks are one position longer.  Spread evenly (l c1 + floor(l x1 / 64)), the starts of a 32-lane
+    // half fall on 31 distinct banks mod 32, and every dword access of round 1 is 2-way; the reference capture's
+    // (c1, x1) = (15, 17) has a layout whose starts are distinct mod 32 in each half (a search over the 16/15 chunk
+    // sequences): 16-position chunks on lanes 8, 10, .., 22 of each half and on lane 31.  LDS_BALANCED_R1 selects
+    // it; the crossing look-up's owner estimate is within one lane of it (every position checked on the host).
+    __host__ __device__ static int r1_start_of(int c1, int x1, int l) {
+        if (LDS_BALANCED_R1 && c1 == 15 && x1 == 17)
+            return 15 * l + min(8, max(0, ((l & 31) - 7) >> 1)) + 9 * (l >> 5) - (l >> 6);
+        return l * c1 + ((l * x1) >> 6);
+    }
     __host__ __device__ static DetGeom of(int Lc) {
         DetGeom g{};
         // Lazy: round 0 covers the first 64 FRAME_LAZY_C0 positions (the reference capture: 1984 of 2961), and
@@ -492,7 +515,9 @@ struct ImMod {
 // single ds_read_b64 (A/B on the reference sweep, profiles/r05/ab/mf_load_forms.txt: 0 -> 1 +0.4 %, -> 2 +0.6 %,
 // conflict cycles 479 -> 351 per item).  The fixed-geometry kernel uses 2; the generic ones 1 (2 spills them at
 // their 168-VGPR budget).
-#define FRAME_MF_B64 2
+#ifndef FRAME_MF_B64
+#define FRAME_MF_B64 3
+#endif
 #define FRAME_MF_B64_GEN 1
 template <int ODD, int FORM, int N>
 __device__ __forceinline__ void lds_readn(const float *p, int s, float (&x)[N]) {
@@ -504,7 +529,10 @@ __device__ __forceinline__ void lds_readn(const float *p, int s, float (&x)[N]) 
 #pragma unroll
     for (int m = 0; m < (N - 1) / 2; ++m) {
         float wx, wy;                                    // floats s + ODD + 2m, s + ODD + 2m + 1
-        if constexpr (FORM == 2) {
+        if constexpr (FORM == 3) {
+            const f2v w = *(volatile lf2c *)(q + m);
+            wx = w.x; wy = w.y;
+        } else if constexpr (FORM == 2) {
             lf2c *qm = q + m;
             opaque(qm);
             const f2v w = *qm;
@@ -597,7 +625,7 @@ __global__ __launch_bounds__(64 * W, FRAME_SYNC_MINW) void frame_sync_kernel(Fra
     const int L = FIX ? FIX_CAP : a.cap_len, Lc = L - 47;       // Packet_Detection length (OFDM.c:663)
     const int nfr = fr_len(FIX ? FIX_ND : a.n_data);
     const int ns = acc_slots(!FIX && a.word_stats);
-    const int imt_len = FIX ? wave_len_for(FIX_ND) / FR_REPS + IMT_EXT : a.imt_len;
+    const int imt_len = FIX ? FIX_IMT_COPIES * (wave_len_for(FIX_ND) / FR_REPS) + IMT_EXT : a.imt_len;
     unsigned long long *acc = smem;                                           // [n_snr][ns]
     float *imt = reinterpret_cast<float *>(acc + a.n_snr * ns);              // imaginary parts, [imt_len]
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -612,7 +640,7 @@ __global__ __launch_bounds__(64 * W, FRAME_SYNC_MINW) void frame_sync_kernel(Fra
     // mod nfilt]; a lane's contiguous reads start below nfilt and run at most IMT_EXT past it); an external
     // capture (ofdm_receiver, one item) its own imaginary parts, imt[n] = Im ext[n], zero past L
     for (int k = threadIdx.x; k < imt_len; k += SYNC_THREADS)
-        imt[k] = !FIX && a.ext ? (k < L ? a.ext[k].y : 0.f) : a.wave[k % (FIX ? imt_len - IMT_EXT : a.im_period)].y;
+        imt[k] = !FIX && a.ext ? (k < L ? a.ext[k].y : 0.f) : a.wave[k % (FIX ? wave_len_for(FIX_ND) / FR_REPS : a.im_period)].y;
     __syncthreads();
     const int lane = threadIdx.x & 63;
 #ifdef OFDM_FRAME_STAMPS
@@ -623,7 +651,7 @@ __global__ __launch_bounds__(64 * W, FRAME_SYNC_MINW) void frame_sync_kernel(Fra
     // in round 1 from B1
     const DetGeom dg = DetGeom::of(Lc);
     const int c0 = dg.c0, c1 = dg.c1, x1 = dg.x1, B1 = dg.B1, R = dg.R;
-    auto r1_start = [c1, x1](int l) { return l * c1 + ((l * x1) >> 6); };    // DetGeom::r1_start
+    auto r1_start = [c1, x1](int l) { return DetGeom::r1_start_of(c1, x1, l); };
     // Items go out in runs of FRAME_ITEM_RUN per wave: wave gw starts with run gw, the runs past the first
     // gridDim.x * SYNC_WAVES come from a per-launch atomic counter, so waves that run fast take more runs.
     // Lane 0 fetches the next run at the first item of the current one (its wait is paid once per run).
@@ -750,7 +778,9 @@ __global__ __launch_bounds__(64 * W, FRAME_SYNC_MINW) void frame_sync_kernel(Fra
                 using LdsF = const __attribute__((address_space(3))) float;
                 // (the period wrap puts part of a 32-lane group on a shifted bank pattern; a timing-only build without
                 // it measured no difference and 19 of 527 conflict cycles per item, profiles/r04/pmc_ab/q_lds_nowrap)
-                LdsF *ti_ = (LdsF *)(imt + im_mod(im0 + n0));
+                // with FIX_IMT_COPIES >= 3 the round's base is reduced once (uniform) and the lanes read a linear run
+                LdsF *ti_ = (LdsF *)(imt + (FIX && FIX_IMT_COPIES >= 3 ? (rho ? im_mod(im0 + B1) + (n0 - B1) : im0 + n0)
+                                                                         : im_mod(im0 + n0)));
                 LdsF *tr_ = (LdsF *)(r + n0);
                 opaque(ti_);
                 opaque(tr_);
@@ -981,6 +1011,7 @@ __global__ __launch_bounds__(64 * W, FRAME_SYNC_MINW) void frame_sync_kernel(Fra
             constexpr int c0 = (32 + MF_RUN - 1) / MF_RUN, c1 = c0 + (128 + MF_RUN - 1) / MF_RUN;
             constexpr int cd = (64 + MF_RUN - 1) / MF_RUN;
             const int n_runs = c1 + cd * n_data;
+            const int im_mf = im_mod(im0 + p - 20 + (wave_len / FR_REPS));      // table index of sample p - 20 (uniform)
             for (int u = lx; u < n_runs; u += 64) {
                 int s0, e;
                 if (u < c0) {
@@ -993,11 +1024,14 @@ __global__ __launch_bounds__(64 * W, FRAME_SYNC_MINW) void frame_sync_kernel(Fra
                 }
                 e = min(e, s0 + MF_RUN);
                 const int n_lo = p + 2 * s0 - 20;                // first sample read
-                if (n_lo >= 0 && p + 2 * (e - 1) < L) {
-                    float xr[MF_W], xi[MF_W];                    // x[k] = sample n_lo + k
-                    const int si = im_mod(im0 + n_lo);
-                    if (par_r) lds_readn<1, MF_FORM>(rbase, off + n_lo, xr); else lds_readn<0, MF_FORM>(rbase, off + n_lo, xr);
-                    if (par_i) lds_readn<1, MF_FORM>(imt, si, xi); else lds_readn<0, MF_FORM>(imt, si, xi);
+                // one run: its window's real and imaginary samples (x[k] = sample n_lo + k) from float parities PR /
+                // PI, then its outputs
+                auto mf_run = [&](auto prc, auto pic) {
+                    constexpr int PR = decltype(prc)::value, PI = decltype(pic)::value;
+                    float xr[MF_W], xi[MF_W];
+                    lds_readn<PR, MF_FORM>(rbase, off + n_lo, xr);
+                    // with FIX_IMT_COPIES >= 3: the pass's uniform base + the lane's offset 2 s0 (< 1,000: inside the copies)
+                    lds_readn<PI, MF_FORM>(imt, FIX && FIX_IMT_COPIES >= 3 ? im_mf + 2 * s0 : im_mod(im0 + n_lo), xi);
 #pragma unroll
                     for (int o = 0; o < MF_RUN; ++o) {           // output at sample n_lo + 2 o + 20
                         if (s0 + o < e) {
@@ -1008,6 +1042,22 @@ __global__ __launch_bounds__(64 * W, FRAME_SYNC_MINW) void frame_sync_kernel(Fra
                                 v.y = fmaf(xi[2 * o + 20 - tt] + xi[2 * o + tt], tv[tt], v.y);
                             }
                             fr[s0 + o] = v;
+                        }
+                    }
+                };
+                using I0 = std::integral_constant<int, 0>;
+                using I1 = std::integral_constant<int, 1>;
+                if (n_lo >= 0 && p + 2 * (e - 1) < L) {
+                    if constexpr (FIX) {
+                        // a generated capture: im0 = rx_start mod nfilt (even) and off = rx_start & 3 have the parity
+                        // of rx_start, so par_i == par_r, and each parity is one straight-line copy of the run (no
+                        // register copies where two load paths would join)
+                        if (par_r) mf_run(I1{}, I1{}); else mf_run(I0{}, I0{});
+                    } else {
+                        if (par_r) {
+                            if (par_i) mf_run(I1{}, I1{}); else mf_run(I1{}, I0{});
+                        } else {
+                            if (par_i) mf_run(I0{}, I1{}); else mf_run(I0{}, I0{});
                         }
                     }
                 } else {
@@ -1274,9 +1324,9 @@ void launch_frame_sym(hipStream_t st, const FrameArgs &a, int cus) {
 // K4b with the reference message's geometry folded (frame_sync_kernel<2, 3008>) in its own translation unit
 // (ofdm_frame_fix.hip), scheduled for ILP without spilling the generic instantiations (A/B +0.4 %,
 // profiles/r04/ab/q_ab_syncilp.txt); its occupancy handle and launcher
-const void *frame_fix_kernel() { return reinterpret_cast<const void *>(&frame_sync_kernel<2, 3008>); }
+const void *frame_fix_kernel() { return reinterpret_cast<const void *>(&frame_sync_kernel<2, 3008, FIX_W>); }
 void launch_frame_fix(hipStream_t st, const FrameArgs &a, dim3 grid, size_t lds) {
-    hipLaunchKernelGGL((frame_sync_kernel<2, 3008>), grid, dim3(SYNC_THREADS), lds, st, a);
+    hipLaunchKernelGGL((frame_sync_kernel<2, 3008, FIX_W>), grid, dim3(64 * FIX_W), lds, st, a);
 }
 }  // namespace ofdm
 #elif defined(OFDM_FRAME_LONG_TU)
@@ -1826,9 +1876,11 @@ static int run_frame_chunk(Ctx *c, FrameArgs &a) {
     const void *ks = fixed ? frame_fix_kernel()
                    : one   ? reinterpret_cast<const void *>(&frame_sync_kernel<0, 0, 1>)
                            : reinterpret_cast<const void *>(&frame_sync_kernel<0, 0>);
-    const int waves = one ? 1 : SYNC_WAVES;
-    const dim3 gs(occupancy_grid(ks, 64 * waves, one ? lds1 : lds, c->cus, (runs + waves - 1) / waves, 1));
-    if (fixed) launch_frame_fix(c->stream, a, gs, lds);
+    const int waves = fixed ? FIX_W : one ? 1 : SYNC_WAVES;
+    // the fixed kernel's table: FIX_IMT_COPIES periods (its own layout, see FIX_W)
+    const size_t lds_f = frame_lds_bytes(a.cap_len, a.n_data, a.n_snr, FIX_IMT_COPIES * a.im_period + IMT_EXT, 0, FIX_W);
+    const dim3 gs(occupancy_grid(ks, 64 * waves, fixed ? lds_f : one ? lds1 : lds, c->cus, (runs + waves - 1) / waves, 1));
+    if (fixed) launch_frame_fix(c->stream, a, gs, lds_f);
     else if (one) hipLaunchKernelGGL((frame_sync_kernel<0, 0, 1>), gs, dim3(64), lds1, c->stream, a);
     else hipLaunchKernelGGL((frame_sync_kernel<0, 0>), gs, dim3(SYNC_THREADS), lds, c->stream, a);
     launch_frame_sym(c->stream, a, c->cus);

@@ -45,7 +45,7 @@ def test_product_kernels_do_not_spill(pkg):
     rows = json.loads(build_lib.RESOURCE_REPORT.read_text())
     names = {x["name"] for x in rows}
     for k in ("ofdm::rx_pack_kernel<0, 0, 0, false>", "ofdm::rx_pack_kernel<2, 0, 0, false>",
-              "ofdm::rx_pack_kernel<2, 0, 1, false>", "ofdm::frame_sync_kernel<2, 3008, 4>", "ofdm::frame_sync_kernel<0, 0, 4>",
+              "ofdm::rx_pack_kernel<2, 0, 1, false>", "ofdm::frame_sync_kernel<2, 3008, 12>", "ofdm::frame_sync_kernel<0, 0, 4>",
               "ofdm::frame_sync_kernel<0, 0, 1>", "ofdm::frame_sym_kernel<false, 2>",
               "ofdm::frame_sym_kernel<false, 0>",
               "ofdm::rx_ls_kernel<1, 1, false>", "ofdm::tx_symbols_kernel<0>"):

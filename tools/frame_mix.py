@@ -40,7 +40,7 @@ sys.path.insert(0, str(ROOT / "tools"))
 sys.path.insert(0, str(PKG))
 from isa_mix import COST, classify  # noqa: E402
 
-SYNC = "_ZN4ofdm17frame_sync_kernelILi2ELi3008ELi4EEEvNS_9FrameArgsE"
+SYNC = "_ZN4ofdm17frame_sync_kernelILi2ELi3008ELi12EEEvNS_9FrameArgsE"
 SYM = "_ZN4ofdm16frame_sym_kernelILb0ELi2EEEvNS_9FrameArgsE"
 CLASSES = ("fast", "slow", "trans", "cnd")
 DYN = {"fma_f32": re.compile(r"^v_(fma|fmac|fmamk|fmaak)_f32"), "mul_f32": re.compile(r"^v_mul_f32"),
@@ -126,6 +126,14 @@ def weights(bbs, passes0: float, run: int = 4):
     for i in range(d0 + 1, target(d0, "s_cbranch_vccnz")):
         if w[i][0]:
             w[i] = (0.0, 1.0)
+    # the matched filter's run is one straight-line copy per float parity of the item (ofdm_frame.hip mf_run): the two
+    # copies (each opening with its run's 28 ds_read_b64) run on half the items each on average
+    mf = [i for i in range(lo, hi + 1) if bbs[i][1] == 2 and sum(op == "ds_read_b64" for op, _ in bbs[i][2]) >= 20]
+    if len(mf) == 2:
+        join = target(mf[1] - 2, "s_branch")
+        assert join and join > mf[1], (mf, join)
+        for i in range(mf[0], join):
+            w[i] = (0.5 * w[i][0], 0.5 * w[i][1])
     return w
 
 
