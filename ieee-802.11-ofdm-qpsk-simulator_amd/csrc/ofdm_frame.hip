@@ -1368,6 +1368,9 @@ __global__ __launch_bounds__(64 * W, FRAME_LONG_MINW) void frame_sync_long_kerne
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     float *rbase = imt + ((a.imt_len + 3) & ~3) + wv * a.region_floats;
     for (int i = threadIdx.x; i < a.n_snr * ns; i += SYNC_THREADS_L) acc[i] = 0ull;
+    // the imaginary parts over one period + LONG_TABLE_REACH (a.imt_len, set by the host): each detection round and
+    // the matched filter reduce one uniform table base, no lane reads across the period wrap (frame_sync_kernel's
+    // FIX_IMT_COPIES)
     for (int k = threadIdx.x; k < a.imt_len; k += SYNC_THREADS_L) imt[k] = a.wave[k % a.im_period].y;
     __syncthreads();
     const int lane = threadIdx.x & 63;
@@ -1411,7 +1414,7 @@ __global__ __launch_bounds__(64 * W, FRAME_LONG_MINW) void frame_sync_long_kerne
             unsigned long long cmask = 0ull;
             if (n0 < n1) {
                 using LdsF = const __attribute__((address_space(3))) float;
-                LdsF *ti_ = (LdsF *)(imt + im_mod(im0 + n0));
+                LdsF *ti_ = (LdsF *)(imt + im_mod(im0 + rho * LW_ROUND) + lx * LW_CHUNK);   // uniform base + lane offset
                 LdsF *tr_ = (LdsF *)(rp + n0);
                 opaque(ti_);
                 opaque(tr_);
@@ -1524,11 +1527,17 @@ __global__ __launch_bounds__(64 * W, FRAME_LONG_MINW) void frame_sync_long_kerne
         }
         const bool sync_fail = cand == 0x7fffffff;
         const int p = sync_fail ? 0 : cand + 10 + 1;
-        // ---- the matched filter's samples [p - 20, p + 2 (nfr - 1) + 10]: resident, or generated again ----
+        // ---- the matched filter's samples [p - 20, p + 2 (nfr - 1) + 10]: resident, or generated again.  After
+        // piece 2 (written from block b0 + LW_ROUND / 4 on) the region still holds piece 1's samples [0, LW_ROUND - 4)
+        // at their piece-1 places and piece 2's samples [2 LW_ROUND, L) at theirs: a window inside either is read
+        // where it lies (a failed sync, p = 0, reads [0, 2 nfr - 10): the low-SNR items that need round 2) ----
         const float *rm = r;
         {
             const int lo = max(p - 20, 0), hi = min(p + 2 * (nfr - 1) + 10, L - 1);
-            if (hi >= res_end || !res1) {
+            const bool in1 = res1 ? hi < res_end : hi < LW_ROUND - 4;
+            const bool in2 = !res1 && lo >= 2 * LW_ROUND;
+            if (in2) rm = r - LW_ROUND;
+            if (!in1 && !in2) {
                 const int s0 = lo & ~3;
                 wave_lds_sync();                              // detection's loads are done
                 capture_blocks(a, wave_len, rbase, (rx_start + s0) >> 2, (rx_start + s0) >> 2, (rx_start + hi) >> 2, lane,
@@ -1555,6 +1564,7 @@ __global__ __launch_bounds__(64 * W, FRAME_LONG_MINW) void frame_sync_long_kerne
         constexpr int c0r = (32 + MF_RUN - 1) / MF_RUN, c1r = c0r + (128 + MF_RUN - 1) / MF_RUN;
         constexpr int cd = (64 + MF_RUN - 1) / MF_RUN;
         const int n_runs = c1r + cd * n_data;
+        const int im_mf = im_mod(im0 + p - 20 + a.im_period);    // table index of sample p - 20 (uniform)
         float2 mfo[LW_MAXP][MF_RUN];
         int mfs[LW_MAXP], mfe[LW_MAXP];
         static_for<0, LW_MAXP>([&](auto pc) {
@@ -1577,7 +1587,7 @@ __global__ __launch_bounds__(64 * W, FRAME_LONG_MINW) void frame_sync_long_kerne
             const int n_lo = p + 2 * s0 - 20;
             if (u < n_runs && n_lo >= 0 && p + 2 * (e - 1) < L) {
                 float xr[MF_W], xi[MF_W];
-                const int si = im_mod(im0 + n_lo);
+                const int si = im_mf + 2 * s0;                                // < 3 periods: inside the copies
                 if (par_r) lds_readn<1, FRAME_MF_B64_LONG>(rm, n_lo, xr); else lds_readn<0, FRAME_MF_B64_LONG>(rm, n_lo, xr);
                 if (par_i) lds_readn<1, FRAME_MF_B64_LONG>(imt, si, xi); else lds_readn<0, FRAME_MF_B64_LONG>(imt, si, xi);
 #pragma unroll
@@ -1694,6 +1704,10 @@ void launch_frame_long(hipStream_t st, const FrameArgs &a, dim3 grid, size_t lds
 // the long-capture kernel's per-wave region (floats): the resident piece (LW_RES samples + capture offset + the last
 // detection lane's block overshoot), which also holds a regenerated matched-filter window and then fr[]
 constexpr int FRAME_LONG_REGION = 4032;
+// the long kernel's imaginary-part table runs LONG_TABLE_REACH floats past one period: a detection round's lanes
+// read up to 63 x 31 + 5 x 16 = 2,033 floats past its base, a matched-filter pass up to 2 x 956 + 29 = 1,941
+// (8 data symbols).  8-symbol frames: 2 blocks x (256 + 15,952 + 4 x 16,128 B) = 161.4 KB of the CU's 160 KiB
+constexpr int LONG_TABLE_REACH = 2048;
 constexpr int FRAME_LONG_MIN_CAP = 4100;     // captures longer than this (frames of >= 5 data symbols) run it
 
 // ======================================================================== host side
@@ -1850,6 +1864,7 @@ static int run_frame_chunk(Ctx *c, FrameArgs &a) {
                          !FRAME_STAMPS_BUILD;
     if (is_long) {
         a.region_floats = FRAME_LONG_REGION;
+        a.imt_len = a.im_period + LONG_TABLE_REACH;           // the long kernel's wrap-free table
         const size_t lds_l = (size_t)a.n_snr * 2 * 8 + (((size_t)a.imt_len * 4 + 15) & ~size_t(15)) +
                              (size_t)SYNC_WAVES * FRAME_LONG_REGION * 4;
         const dim3 gl(occupancy_grid(frame_long_kernel(), SYNC_THREADS, lds_l, c->cus, (runs + SYNC_WAVES - 1) / SYNC_WAVES, 1));
