@@ -170,139 +170,6 @@ void fft64_lds_kernel(const float2 *in, float2 *out, int64_t n) {   // in == out
     }
 }
 
-// K1 with SIXTEEN LANES PER TRANSFORM: a wave owns K1R_TPW = 4 transforms (2 KB, contiguous in
-// HBM), a 16-lane DPP row each, every lane busy; 2 KB per wave is the copy shape that moves 6.23 TB/s on this box
-// against 6.05 for the 4 KB of fft64_lds_kernel (tools/ubench_copy.hip, profiles/r05/ab/copy_ceiling.txt).
-// 64 = 4 x 4 x 4, radix-4 DIF in three in-register stages with two LDS transposes between them:
-//   stage 1, lane (t, j):      y_r[j] = W64^{jr} sum_q x[j + 16 q] W4^{qr}                (r < 4; x read from LDS)
-//   stage 2, lane (t, r, a):   z_m1[a] = W16^{a m1} sum_b y_r[a + 4 b] W4^{b m1}           (j = a + 4 b)
-//   stage 3, lane (t, r, m1):  X[r + 4 m1 + 16 m2] = sum_a z_m1[a] W4^{a m2}
-// Every LDS access is a ds_read_b64 / ds_write_b64 whose 32-lane halves hit 32 distinct 8-byte slots mod 64 banks:
-// the slots are XOR-permuted per transform parity (t_lo) and per index (the bijections noted at each layout);
-// the HBM sides are fft64_lds_kernel's (LDS-DMA loads, 16-B non-temporal stores, 1 KB contiguous per instruction).
-constexpr int K1R_TPW = 4;
-__device__ __forceinline__ float2 k1r_bfly(float2 x0, float2 x1, float2 x2, float2 x3, int m, bool inv) {
-    // output m of the 4-point DFT sum_q x_q W4^{qm} (W4 = -j forward, +j inverse)
-    const float2 t0 = cadd(x0, x2), t1 = csub(x0, x2), t2 = cadd(x1, x3), t3 = csub(x1, x3);
-    if (m == 0) return cadd(t0, t2);
-    if (m == 2) return csub(t0, t2);
-    const bool minus_j = (m == 1) != inv;                        // t1 - j t3 (m = 1 forward, m = 3 inverse)
-    return minus_j ? make_float2(t1.x + t3.y, t1.y - t3.x) : make_float2(t1.x - t3.y, t1.y + t3.x);
-}
-template <bool INV>
-__device__ __forceinline__ float2 k1r_tw(float2 v, int e) {   // v W64^e (e < 64), exact table constants
-    const float c = kCos64[e], s = INV ? kSin64[e] : -kSin64[e];
-    return make_float2(fmaf(v.x, c, -v.y * s), fmaf(v.x, s, v.y * c));
-}
-template <bool INV, int CONV>
-__global__ __launch_bounds__(256) void fft64_row_kernel(const float2 *in, float2 *out, int64_t n) {   // in == out allowed
-    __shared__ __attribute__((aligned(16))) float4 buf[4][32 * K1R_TPW];
-    typedef __attribute__((address_space(3))) f2v lf2w;
-    typedef const __attribute__((address_space(3))) f2v lf2r;
-    typedef const __attribute__((address_space(3))) f4v lf4c;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t t_base = ((int64_t)blockIdx.x * 4 + wv) * K1R_TPW;
-    const int64_t avail = (n - t_base) * 32;                           // chunks of this wave that exist (<= 0: idle)
-    float4 *wb = buf[wv];
-    lf2w *slots = (lf2w *)wb;                                          // 8-byte slots: transform t at 64 t
-    const float4 *src = reinterpret_cast<const float4 *>(in) + t_base * 32;
-    // loads: LDS chunk p of transform t holds source chunk p ^ 8 t_lo (complex n at slot n ^ 16 t_lo)
-#pragma unroll
-    for (int s = 0; s < K1R_TPW / 2; ++s) {
-        const int P = 64 * s + lane, t = P >> 5, c = (P & 31) ^ (8 * (t & 1));
-        if (t * 32 + c < avail)
-            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(src + t * 32 + c),
-                                             (__attribute__((address_space(3))) void *)(wb + 64 * s), 16, 0, 2);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                  // this wave's DMA has landed (wave-private)
-    const int t = lane >> 4, tl = t & 1, j = lane & 15;
-    lf2w *ts = slots + 64 * t;
-    // ---- stage 1, lane (t, j): x[j + 16 q] at slot (j + 16 q) ^ 16 tl (fixed q: (tl, j) -> 5 distinct low bits)
-    float2 x[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const f2v v = *(lf2r *)(ts + ((j + 16 * q) ^ (16 * tl)));
-        const float sg = ((!INV || CONV == OFDM_CONV_C) && (j & 1)) ? -1.0f : 1.0f;   // (-1)^n, n parity = j's (D5)
-        x[q] = make_float2(sg * v.x, sg * v.y);
-    }
-    float2 y[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) y[r] = k1r_tw<INV>(k1r_bfly(x[0], x[1], x[2], x[3], r, INV), j * r);
-    // every lane's x reads precede the writes that reuse the slots (one wave: LDS operations complete in order)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // ---- transpose 1: y_r[a + 4 b] at slot bits (a | (b ^ r) << 2 | (r0 ^ tl) << 4 | r1 << 5): a writer's fixed r and
-    // a reader's fixed b both leave 5 distinct low bits over their half-wave
-    {
-        const int a = j & 3, b = j >> 2;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            f2v w; w.x = y[r].x; w.y = y[r].y;
-            ts[a | ((b ^ r) << 2) | (((r & 1) ^ tl) << 4) | ((r >> 1) << 5)] = w;
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // ---- stage 2, lane (t, r, a) = (t, j >> 2, j & 3)
-    const int r = j >> 2, a = j & 3;
-    float2 v[4];
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-        const f2v u = *(lf2r *)(ts + (a | ((b ^ r) << 2) | (((r & 1) ^ tl) << 4) | ((r >> 1) << 5)));
-        v[b] = make_float2(u.x, u.y);
-    }
-    float2 z[4];
-#pragma unroll
-    for (int m1 = 0; m1 < 4; ++m1) z[m1] = k1r_tw<INV>(k1r_bfly(v[0], v[1], v[2], v[3], m1, INV), 4 * a * m1);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // ---- transpose 2: z_m1[a] at slot bits (r | (a ^ m1) << 2 | (tl ^ a0) << 4 | a1 << 5)
-#pragma unroll
-    for (int m1 = 0; m1 < 4; ++m1) {
-        f2v w; w.x = z[m1].x; w.y = z[m1].y;
-        ts[r | ((a ^ m1) << 2) | ((tl ^ (a & 1)) << 4) | ((a >> 1) << 5)] = w;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // ---- stage 3, lane (t, r, m1) = (t, j & 3, j >> 2): bins k = r + 4 m1 + 16 m2
-    {
-        const int r3 = j & 3, m1 = j >> 2;
-        float2 w4[4];
-#pragma unroll
-        for (int a3 = 0; a3 < 4; ++a3) {
-            const f2v u = *(lf2r *)(ts + (r3 | ((a3 ^ m1) << 2) | ((tl ^ (a3 & 1)) << 4) | ((a3 >> 1) << 5)));
-            w4[a3] = make_float2(u.x, u.y);
-        }
-        const float scale = INV ? ((r3 & 1) ? -1.0f / 64.0f : 1.0f / 64.0f) : 1.0f;   // (-1)^k / 64, k parity = r's
-        float2 X[4];
-#pragma unroll
-        for (int m2 = 0; m2 < 4; ++m2) X[m2] = cscale(k1r_bfly(w4[0], w4[1], w4[2], w4[3], m2, INV), scale);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // bin k at slot k ^ 16 tl: a store chunk (bins 2c, 2c + 1) stays one aligned 16-B pair
-#pragma unroll
-        for (int m2 = 0; m2 < 4; ++m2) {
-            f2v w; w.x = X[m2].x; w.y = X[m2].y;
-            ts[(r3 + 4 * m1 + 16 * m2) ^ (16 * tl)] = w;
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    float4 *dst = reinterpret_cast<float4 *>(out) + t_base * 32;
-#pragma unroll
-    for (int s = 0; s < K1R_TPW / 2; ++s) {
-        const int g = 64 * s + lane, tg = g >> 5, c = g & 31;
-        const f4v w = *(lf4c *)(wb + 32 * tg + (c ^ (8 * (tg & 1))));
-        if (g < avail) __builtin_nontemporal_store(w, reinterpret_cast<f4v *>(dst) + g);
-    }
-}
-
 // ======================================================================== K2: Tx builder
 // One lane = one data symbol (tx_symbol, ofdm_rxcommon.h: bits -> QPSK -> map + pilots -> ifft -> CP -> HBM).
 template <int CONV>
@@ -810,17 +677,10 @@ __global__ __launch_bounds__(256, OFDM_RX_IDEAL_WAVES) void rx_ideal_kernel(RxAr
 }
 
 // ======================================================================== launchers
-#ifndef OFDM_K1_ROWS
-#define OFDM_K1_ROWS 0
-#endif
+// (16 lanes per transform at 2 KB per wave, fft64_row_kernel: correct and LDS-conflict-free but -10 %, round 6,
+// profiles/r06/k1/ab_rows.txt; in history at commit f61d0a7)
 template <bool INV>
 static void launch_fft_conv(int conv, hipStream_t st, const float2 *in, float2 *out, int64_t n) {
-    if (OFDM_K1_ROWS) {                                  // 16 lanes per transform (fft64_row_kernel)
-        const dim3 gr((unsigned)((n + 4 * K1R_TPW - 1) / (4 * K1R_TPW)));
-        if (conv == OFDM_CONV_C) hipLaunchKernelGGL((fft64_row_kernel<INV, OFDM_CONV_C>), gr, dim3(256), 0, st, in, out, n);
-        else hipLaunchKernelGGL((fft64_row_kernel<INV, OFDM_CONV_MATLAB>), gr, dim3(256), 0, st, in, out, n);
-        return;
-    }
     const dim3 gl((unsigned)((n + 4 * OFDM_K1_TPW - 1) / (4 * OFDM_K1_TPW)));
     if (conv == OFDM_CONV_C) hipLaunchKernelGGL((fft64_lds_kernel<INV, OFDM_CONV_C>), gl, dim3(256), 0, st, in, out, n);
     else hipLaunchKernelGGL((fft64_lds_kernel<INV, OFDM_CONV_MATLAB>), gl, dim3(256), 0, st, in, out, n);
