@@ -120,11 +120,12 @@ def issue_cap(pmc: dict, frac: float) -> dict:
                                     "%d waves/SIMD, the unclassified instructions split fast / slow / cndmask as in "
                                     "the classified model of frame's sync kernel (%s); range: all slow .. all fast"
                                     % (m["waves_per_simd"], m["split_source"])}
-    if m.get("method") == "classified":  # tools/frame_mix.py: every VALU instruction classified, blocks weighted
+    if m.get("method") == "classified":  # tools/frame_mix.py / frame8_mix.py: every VALU instruction classified
         return {"issue_model_cap_frac": m["cap_frac"], "frac_of_issue_model_cap": frac / m["cap_frac"],
                 "issue_model_note": "cap = 2 x VALU / class-priced SIMD cycles at %d waves/SIMD of both kernels' "
                                     "assembly, blocks weighted per item (undecided fraction %.3f fitted to the "
-                                    "measured SQ_INSTS_VALU)" % (m["waves_per_simd"], m["undecided_fraction"])}
+                                    "measured %s)" % (m["waves_per_simd"], m["undecided_fraction"],
+                                                      m.get("fit", "SQ_INSTS_VALU"))}
     return {"issue_model_cap_frac": m["cap_frac"], "frac_of_issue_model_cap": frac / m["cap_frac"],
             "issue_model_note": "cap = 2 x loop VALU / class-priced SIMD cycles at %d waves/SIMD (modelled)"
                                 % m["waves_per_simd"]}

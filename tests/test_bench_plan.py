@@ -529,3 +529,19 @@ def test_pmc_trace_fallback_matches_stats(tmp_path):
     assert a and a.keys() == b.keys()
     for k in a:
         assert a[k]["calls"] == b[k]["calls"] and a[k]["total_ns"] == pytest.approx(b[k]["total_ns"])
+
+
+def test_frame8_classified_cap():
+    """tools/frame8_mix.py classifies frame_sync_long_kernel's own assembly (instructions attributed
+    to kernel statements through the -g build's DWARF inlining records) and weights it per item.  On the committed
+    round-6 PMC record the undecided fraction it fits from the FMA count agrees with the CPU simulation of the kernel's
+    rules (tests/golden/frame8_path_rates.json), and the cap lies between the all-slow and all-fast pricing."""
+    sys.path.insert(0, str(ROOT / "tools"))
+    import frame8_mix
+    d = ROOT / "profiles" / "r06" / "pmc" / "frame8"
+    m = frame8_mix.model([d / "pmc_7", d / "pmc_2"], 32_000_000 / 8, 2)
+    assert abs(m["undecided_fraction"] - m["undecided_fraction_simulated"]) < 0.05
+    assert abs(m["g_build_instr_delta"]) < 16
+    assert 0.58 < m["sync"]["cap_frac"] < 0.71 and 0.55 < m["cap_frac"] < 0.75
+    assert abs(m["sync"]["class_check_per_item"]["mul_f32"]["model"] /
+               m["sync"]["class_check_per_item"]["mul_f32"]["measured"] - 1) < 0.1
