@@ -73,6 +73,33 @@ def rounds_decision(m, limit):
     return True, int(valid[0]) + LEN_RRC_RX + 1
 
 
+def packet_selection(m, thr=0.75):
+    """Packet_Selection (OFDM.c:685-771) over the whole of M with the threshold as a parameter: the first front
+    (a crossing more than 300 positions past the previous one) but the last whose M[front + 230] crosses too ->
+    front + len_RRC_rx + 1; 0 when none does.  tests/test_gpu_frame.py moves `thr` to show that a packet_idx on
+    which the GPU and the oracle differ sits on the threshold."""
+    idx = np.nonzero(m > thr)[0]
+    prev = np.concatenate([[-1], idx[:-1]])
+    fronts = idx[(idx - prev) > 300]
+    for f in fronts[:-1]:
+        if f + 230 < len(m) and m[f + 230] > thr:
+            return int(f) + LEN_RRC_RX + 1
+    return 0
+
+
+@pytest.mark.parametrize("snr_db", [0.0, 6.0, 9.0, 12.0, 30.0])
+def test_packet_selection_helper_is_the_references(reflib, snr_db):
+    wave = reflib.waveform().astype(np.complex128)
+    L = int(0.307 * len(wave))
+    rng = np.random.default_rng(int(snr_db * 10) + 7)
+    sigma = np.sqrt(np.mean(np.abs(wave) ** 2) / 10 ** (snr_db / 10))
+    for _ in range(200):
+        s = int(rng.integers(0, len(wave) - L))
+        m = corr_out(wave[s:s + L] + sigma * rng.standard_normal(L))
+        ref = reflib.lib.ref_packet_selection(m.ctypes.data_as(C.c_void_p), len(m))
+        assert packet_selection(m) == ref, (snr_db, s)
+
+
 @pytest.mark.parametrize("snr_db", [0.0, 6.0, 10.0, 16.0, 30.0])
 def test_long_frames_two_round_decision_is_the_references(oracle, reflib, snr_db):
     msg = (b"lazy rounds for the long-capture kernel: two frame periods decide most trials. " * 2)[:96]
