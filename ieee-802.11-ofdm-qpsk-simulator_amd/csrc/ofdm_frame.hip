@@ -1862,6 +1862,9 @@ static int run_frame_chunk(Ctx *c, FrameArgs &a) {
                          !a.dbg_ints && !a.dbg_bits && !a.dbg_eq && !a.dbg_corr && !a.dbg_frame && !a.word_stats &&
                          2 * fr_len(a.n_data) + 40 <= FRAME_LONG_REGION && !getenv("OFDM_FRAME_NO_LONG") &&
                          !FRAME_STAMPS_BUILD;
+    // every capture routed here has Lc > 2 x 64 x 31: the long kernel always runs three detection rounds (its R == 2
+    // branches are unreachable; they stay so that the PMC-certified code object does not move)
+    static_assert(FRAME_LONG_MIN_CAP - 47 >= 2 * 64 * 31, "long captures take three detection rounds");
     if (is_long) {
         a.region_floats = FRAME_LONG_REGION;
         a.imt_len = a.im_period + LONG_TABLE_REACH;           // the long kernel's wrap-free table

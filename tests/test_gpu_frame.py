@@ -109,17 +109,11 @@ def test_frame_sweep_vs_oracle(engine, oracle, pkg):
     o, op = oracle.frame_sweep(oracle.cfg(payload="message"), snrs, 0, n, "c", dump_pidx=True)
     agree = np.mean(gp == op)
     assert agree > 0.995, agree
-    # every packet_idx on which they differ sits on Packet_Selection's 0.75 threshold: on that trial's capture (the
-    # sweep's own streams, test_sweep_trial_equals_receiver_of_ota) the reference's selection moves when the
-    # threshold moves by 0.1 % -- fp32 sliding sums (GPU) against double ones (oracle), not a different rule
-    from test_lazy_rule import corr_out, packet_selection  # noqa: PLC0415
+    # every packet_idx on which they differ sits on Packet_Selection's 0.75 threshold (fp32 sliding sums on the GPU,
+    # double ones in the oracle), not on a different rule
+    from conftest import off_threshold_pidx_mismatches  # noqa: PLC0415
     w = engine.transmitter("c", "message")
-    for q, t in np.argwhere(gp != op):
-        rs = int(oracle.philox([int(t), 0, 0, 0x5B000000 | int(q)], [0x80211A, 0])[0] % (9800 - 3008))
-        ota = engine.transmission_over_air(w, snrs[q], seed=0x80211A, trial=int(t), snr_index=int(q))
-        m = corr_out(ota[rs:rs + 3008].astype(np.complex128))
-        moved = {packet_selection(m, 0.75 * (1 + d)) for d in np.linspace(-1e-3, 1e-3, 21)}
-        assert len(moved) > 1 and {int(gp[q, t]), int(op[q, t])} & moved, (q, t, gp[q, t], op[q, t], moved)
+    assert off_threshold_pidx_mismatches(engine, oracle, w, snrs, gp, op, 3008) == []
     assert np.array_equal(g[:, 0], o[:, 0])
     assert np.all(np.abs(g[:, 3] - o[:, 3]) <= 96 * np.sum(gp != op, axis=1) + 2)
     assert np.all(np.abs(g[:, 5] - o[:, 5]) <= np.sum(gp != op, axis=1))

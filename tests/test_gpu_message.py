@@ -89,6 +89,11 @@ def test_frame_sweep_vs_oracle(msg_engine, msg_oracle, pkg):
     g, gp = msg_engine.frame_sweep(cfg, snrs, n, want_packet_idx=True)
     o, op = msg_oracle.frame_sweep(msg_oracle.cfg(payload="message"), snrs, 0, n, "c", dump_pidx=True)
     assert np.mean(gp == op) > 0.99
+    from conftest import off_threshold_pidx_mismatches  # noqa: PLC0415
+    from ofdm_amd import abi  # noqa: PLC0415
+    w = msg_engine.transmitter("c", "message")
+    nd = -(-8 * len(MSG) // 96)
+    assert off_threshold_pidx_mismatches(msg_engine, msg_oracle, w, snrs, gp, op, abi.capture_len(nd)) == []
     for k in (0, 1, 2, 6):                                            # frames, symbols, bits, evm terms
         assert np.array_equal(g[:, k], o[:, k])
     assert g[0, 1] == 5 * n and g[0, 2] == 480 * n
@@ -156,6 +161,8 @@ def test_frame_sweep_vs_oracle_lengths(msg_engine, oracle, pkg, msg):
         g, gp = msg_engine.frame_sweep(cfg, snrs, n, want_packet_idx=True)
         r, rp = oracle.frame_sweep(oracle.cfg(payload="message"), snrs, 0, n, "c", dump_pidx=True)
         assert np.mean(gp == rp) > 0.99
+        from conftest import off_threshold_pidx_mismatches  # noqa: PLC0415
+        assert off_threshold_pidx_mismatches(msg_engine, oracle, w, snrs, gp, rp, L) == []
         for k in (0, 1, 2, 6):                                         # frames, symbols, bits, evm terms
             assert np.array_equal(g[:, k], r[:, k])
         assert g[0, 1] == nd * n and g[0, 2] == 96 * nd * n
