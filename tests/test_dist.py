@@ -1,4 +1,4 @@
-"""Multi-process path on CPU (gloo, world_size 2): counter-range sharding + ONE all-reduce of the
+"""Multi-process path on CPU (gloo, world_size 2 and 4): counter-range sharding + ONE all-reduce of the
 int64 counters gives exactly the single-process result.  Per-rank counters come from
 the oracle (test data source); the GPU ranks use the same dist helpers over RCCL."""
 import json
@@ -47,14 +47,15 @@ def _worker(rank, world, port, mode, n, snrs, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["strong", "weak"])
-def test_two_rank_allreduce_equals_single(tmp_path, oracle, mode):
+@pytest.mark.parametrize("mode,world,n", [("strong", 2, 96), ("weak", 2, 96), ("strong", 4, 101), ("weak", 4, 100)])
+def test_ranks_allreduce_equals_single(tmp_path, oracle, mode, world, n):
+    """world 2, and world 4 (a rehearsal of more ranks than the one-GPU box can run over RCCL) with a frame count
+    the strong split cannot divide evenly: the summed shards equal one process's sweep bit for bit"""
     snrs = [0.0, 4.0, 8.0]
-    n = 96
     out = tmp_path / "c.npy"
-    mp.spawn(_worker, args=(2, _free_port(), mode, n, snrs, str(out)), nprocs=2, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), mode, n, snrs, str(out)), nprocs=world, join=True)
     got = np.load(out)
-    ref = oracle.symbol_sweep(oracle.cfg(), snrs, 0, n)
+    ref = oracle.symbol_sweep(oracle.cfg(), snrs, 0, n if mode == "strong" else (n // world) * world)
     assert np.array_equal(got, ref)
 
 
