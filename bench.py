@@ -110,24 +110,24 @@ def issue_cap(pmc: dict, frac: float) -> dict:
         return {"issue_model_cap_frac": lo, "issue_model_cap_frac_range": [lo, hi],
                 "frac_of_issue_model_cap": frac / lo, "frac_of_issue_model_cap_range": [frac / hi, frac / lo],
                 "issue_model_note": "cap = 2 x VALU / SIMD cycles of the dynamic class mix (PMC class counters) at "
-                                    "%d waves/SIMD, unclassified instructions priced slow (cap) or fast (upper end)"
+                                    "%s waves/SIMD, unclassified instructions priced slow (cap) or fast (upper end)"
                                     % m["waves_per_simd"]}
     if m.get("method") == "dynamic_split":   # tools/mix_cap.py --split-from: a point estimate inside that range
         lo, hi = m["cap_frac_range"]
         return {"issue_model_cap_frac": m["cap_frac"], "issue_model_cap_frac_range": [lo, hi],
                 "frac_of_issue_model_cap": frac / m["cap_frac"], "frac_of_issue_model_cap_range": [frac / hi, frac / lo],
                 "issue_model_note": "cap = 2 x VALU / SIMD cycles of the dynamic class mix (PMC class counters) at "
-                                    "%d waves/SIMD, the unclassified instructions split fast / slow / cndmask as in "
+                                    "%s waves/SIMD, the unclassified instructions split fast / slow / cndmask as in "
                                     "the classified model of frame's sync kernel (%s); range: all slow .. all fast"
                                     % (m["waves_per_simd"], m["split_source"])}
     if m.get("method") == "classified":  # tools/frame_mix.py / frame8_mix.py: every VALU instruction classified
         return {"issue_model_cap_frac": m["cap_frac"], "frac_of_issue_model_cap": frac / m["cap_frac"],
-                "issue_model_note": "cap = 2 x VALU / class-priced SIMD cycles at %d waves/SIMD of both kernels' "
+                "issue_model_note": "cap = 2 x VALU / class-priced SIMD cycles at %s waves/SIMD of both kernels' "
                                     "assembly, blocks weighted per item (undecided fraction %.3f fitted to the "
                                     "measured %s)" % (m["waves_per_simd"], m["undecided_fraction"],
                                                       m.get("fit", "SQ_INSTS_VALU"))}
     return {"issue_model_cap_frac": m["cap_frac"], "frac_of_issue_model_cap": frac / m["cap_frac"],
-            "issue_model_note": "cap = 2 x loop VALU / class-priced SIMD cycles at %d waves/SIMD (modelled)"
+            "issue_model_note": "cap = 2 x loop VALU / class-priced SIMD cycles at %s waves/SIMD (modelled)"
                                 % m["waves_per_simd"]}
 
 

@@ -378,6 +378,12 @@ constexpr int SYM_THREADS = 256;    // frame_sym_kernel block: its items per blo
 constexpr size_t FRAME_LDS_PER_CU = 160 * 1024;
 constexpr int SYNC_WAVES = FRAME_SYNC_WAVES;
 constexpr int SYNC_THREADS = 64 * SYNC_WAVES;
+// frame_sync_long_kernel's block: 9 waves, one block per CU (9 x 16,128 B of capture pieces + one 15,952-B table =
+// 161 KB of LDS), at most 168 VGPRs, so one SIMD in four runs a third wave.  Round 6 A/B
+// (profiles/r06/frame/ab_long9.txt): 4-wave blocks (two per CU, 2 waves on every SIMD) 8.02-8.05e8, 9-wave blocks
+// 8.37-8.40e8 (+4.4 %), every counter and packet_idx unchanged.  Ten waves do not fit.
+constexpr int LONG_W = 9;
+#define FRAME_LONG_MINW 3
 constexpr int IMT_EXT = 128;         // table slack past one waveform copy: a lane's longest contiguous read
 // The fixed-geometry kernel's layout: FIX_W waves per block sharing FIX_IMT_COPIES consecutive
 // copies of the imaginary-part period.  With one copy every lane reduces its own table index mod the period, and the
@@ -1354,7 +1360,6 @@ constexpr int LW_CHUNK = 31;
 constexpr int LW_ROUND = 64 * LW_CHUNK;              // 1,984 positions per round
 constexpr int LW_RES = 2 * LW_ROUND + 48;             // resident capture samples (rounds 0 and 1 and their windows)
 constexpr int LW_MAXP = 3;                            // matched-filter passes of 64 runs (33 + 13 nd <= 137 runs)
-#define FRAME_LONG_MINW 2
 #define FRAME_MF_B64_LONG FRAME_MF_B64_GEN   // lds_readn form of the long kernel's matched filter
 template <int W>
 __global__ __launch_bounds__(64 * W, FRAME_LONG_MINW) void frame_sync_long_kernel(FrameArgs a) {
@@ -1690,9 +1695,9 @@ __global__ __launch_bounds__(64 * W, FRAME_LONG_MINW) void frame_sync_long_kerne
 }
 
 // launcher and occupancy handle (ofdm_frame_long.hip)
-const void *frame_long_kernel() { return reinterpret_cast<const void *>(&frame_sync_long_kernel<SYNC_WAVES>); }
+const void *frame_long_kernel() { return reinterpret_cast<const void *>(&frame_sync_long_kernel<LONG_W>); }
 void launch_frame_long(hipStream_t st, const FrameArgs &a, dim3 grid, size_t lds) {
-    hipLaunchKernelGGL((frame_sync_long_kernel<SYNC_WAVES>), grid, dim3(SYNC_THREADS), lds, st, a);
+    hipLaunchKernelGGL((frame_sync_long_kernel<LONG_W>), grid, dim3(64 * LONG_W), lds, st, a);
 }
 }  // namespace ofdm
 #else
@@ -1869,8 +1874,8 @@ static int run_frame_chunk(Ctx *c, FrameArgs &a) {
         a.region_floats = FRAME_LONG_REGION;
         a.imt_len = a.im_period + LONG_TABLE_REACH;           // the long kernel's wrap-free table
         const size_t lds_l = (size_t)a.n_snr * 2 * 8 + (((size_t)a.imt_len * 4 + 15) & ~size_t(15)) +
-                             (size_t)SYNC_WAVES * FRAME_LONG_REGION * 4;
-        const dim3 gl(occupancy_grid(frame_long_kernel(), SYNC_THREADS, lds_l, c->cus, (runs + SYNC_WAVES - 1) / SYNC_WAVES, 1));
+                             (size_t)LONG_W * FRAME_LONG_REGION * 4;
+        const dim3 gl(occupancy_grid(frame_long_kernel(), 64 * LONG_W, lds_l, c->cus, (runs + LONG_W - 1) / LONG_W, 1));
         launch_frame_long(c->stream, a, gl, lds_l);
         launch_frame_sym(c->stream, a, c->cus);
         HIPOK(hipGetLastError());

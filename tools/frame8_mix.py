@@ -3,7 +3,7 @@
 item 3: every VALU instruction of the long kernel's gfx950 code classified (tools/isa_mix.py classes and costs) and
 weighted by how often a (trial, SNR) item executes it.
 
-usage: python tools/frame8_mix.py <pmc dir>... [--items N] [--waves 2] [--record]
+usage: python tools/frame8_mix.py <pmc dir>... [--items N] [--waves 3,2,2,2] [--record]
 
 frame_mix.py (the reference frame's sync kernel) finds its phases by code patterns; the long kernel's 1,500 blocks
 (three capture call sites, three detection rounds, unrolled matched-filter passes with their per-instant fallbacks)
@@ -50,7 +50,7 @@ sys.path.insert(0, str(PKG))
 from isa_mix import COST, classify  # noqa: E402
 import frame_mix  # noqa: E402
 
-LONG = "_ZN4ofdm22frame_sync_long_kernelILi4EEEvNS_9FrameArgsE"
+LONG = "_ZN4ofdm22frame_sync_long_kernelILi9EEEvNS_9FrameArgsE"
 SYM = "_ZN4ofdm16frame_sym_kernelILb0ELi0EEEvNS_9FrameArgsE"
 CLASSES = ("fast", "slow", "trans", "cnd")
 LLVM = Path("/opt/rocm/lib/llvm/bin")
@@ -257,7 +257,7 @@ def tally(ins, w):
     return cls
 
 
-def model(dirs, items: float, waves: int) -> dict:
+def model(dirs, items: float, waves="3,2,2,2") -> dict:
     rates = json.loads((ROOT / "tests" / "golden" / "frame8_path_rates.json").read_text())
     g, u_sim = rates["grid_mean"]["regen"], 1.0 - rates["grid_mean"]["decided"]
     a = anchors()
@@ -299,9 +299,14 @@ def model(dirs, items: float, waves: int) -> dict:
     ycls, _, _ = frame_mix.tally(ybb, {i: (1.0, 0.0) for i, b in enumerate(ybb) if b[1] >= 1})
     vy = my["SQ_INSTS_VALU"] / items
     ny = {k: vy * ycls[k][0] / ycls["valu"][0] for k in CLASSES}
-    cost = COST[waves]
-    cyc_s = sum(cost[k] * n[k] for k in CLASSES)
-    cyc_y = sum(cost[k] * ny[k] for k in CLASSES)
+    # waves: the sync kernel's waves on each of a CU's four SIMDs (9-wave blocks, one per CU: 3, 2, 2, 2).  Items are
+    # handed out dynamically, so the chip's cap is the mean of the SIMDs' caps; the symbol kernel runs 2 per SIMD
+    simds = [int(x) for x in str(waves).split(",")]
+    cyc_y = sum(COST[2][k] * ny[k] for k in CLASSES)
+    cyc_by = {w: sum(COST[w][k] * n[k] for k in CLASSES) for w in set(simds)}
+    cyc_s = sum(cyc_by[w] for w in simds) / len(simds)
+    cap_s = sum(2 * v / cyc_by[w] for w in simds) / len(simds)
+    cap = sum(2 * (v + vy) / (cyc_by[w] + cyc_y) for w in simds) / len(simds)
     checks = {}
     for k, rx in frame_mix.DYN.items():
         d0, d1 = dyn(rx)
@@ -315,15 +320,15 @@ def model(dirs, items: float, waves: int) -> dict:
         "anchors": a,
         "sync": {"kernel": LONG, "valu_per_item": v, "classes_per_item": {k: n[k] for k in CLASSES},
                  "covered_by_class_counters": covered / v, "uncovered_split": share,
-                 "priced_cycles_per_item": cyc_s, "cap_frac": 2 * v / cyc_s, "class_check_per_item": checks},
+                 "priced_cycles_per_item": cyc_s, "cap_frac": cap_s, "class_check_per_item": checks},
         "sym": {"kernel": SYM, "valu_per_item": vy, "classes_per_item": ny, "priced_cycles_per_item": cyc_y,
                 "cap_frac": 2 * vy / cyc_y},
-        "cap_frac": 2 * (v + vy) / (cyc_s + cyc_y)}
+        "cap_frac": cap}
 
 
 def main(argv):
     dirs = [x for x in argv if not x.startswith("--") and Path(x).is_dir()]
-    waves = int(argv[argv.index("--waves") + 1]) if "--waves" in argv else 2
+    waves = argv[argv.index("--waves") + 1] if "--waves" in argv else "3,2,2,2"
     summary_p = ROOT / "profiles" / "pmc_summary.json"
     if "--items" in argv:
         items = float(argv[argv.index("--items") + 1])
