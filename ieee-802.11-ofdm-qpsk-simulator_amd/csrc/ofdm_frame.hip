@@ -378,11 +378,12 @@ constexpr int SYM_THREADS = 256;    // frame_sym_kernel block: its items per blo
 constexpr size_t FRAME_LDS_PER_CU = 160 * 1024;
 constexpr int SYNC_WAVES = FRAME_SYNC_WAVES;
 constexpr int SYNC_THREADS = 64 * SYNC_WAVES;
-// frame_sync_long_kernel's block: 9 waves, one block per CU (9 x 16,128 B of capture pieces + one 15,952-B table =
-// 161 KB of LDS), at most 168 VGPRs, so one SIMD in four runs a third wave.  Round 6 A/B
-// (profiles/r06/frame/ab_long9.txt): 4-wave blocks (two per CU, 2 waves on every SIMD) 8.02-8.05e8, 9-wave blocks
-// 8.37-8.40e8 (+4.4 %), every counter and packet_idx unchanged.  Ten waves do not fit.
-constexpr int LONG_W = 9;
+// frame_sync_long_kernel's block: 12 waves, one block per CU (12 x 12,288 B of capture rings + one 15,952-B table +
+// 256 B = 163,664 B of the CU's 163,840), at most 168 VGPRs: 3 waves on every SIMD.  Round 6 A/Bs: 4-wave blocks with
+// two rounds resident (two blocks per CU, 2 waves per SIMD) 8.02-8.05e8; 9-wave blocks, two rounds resident, 3, 2, 2, 2
+// waves per SIMD 8.37-8.40e8 (profiles/r06/frame/ab_long9.txt); 12-wave blocks, one round resident 8.58-8.62e8
+// (ab_long12.txt); 12-wave blocks with the capture ring 8.76-8.78e8 (ab_ring.txt); every counter and packet_idx unchanged.
+constexpr int LONG_W = 12;
 #define FRAME_LONG_MINW 3
 constexpr int IMT_EXT = 128;         // table slack past one waveform copy: a lane's longest contiguous read
 // The fixed-geometry kernel's layout: FIX_W waves per block sharing FIX_IMT_COPIES consecutive
@@ -559,7 +560,10 @@ __device__ __forceinline__ void lds_readn(const float *p, int s, float (&x)[N]) 
 
 // Capture Philox blocks bs..be (block b = waveform samples 4b..4b+3; b0 = the capture's first block) into the
 // wave's region: the real parts of the clean waveform plus real AWGN (OFDM.c:622-655, D7).
-template <typename A>
+// RING > 0 (frame_sync_long_kernel): the region is a ring of RING floats (a multiple of 4) plus EXT mirrored floats --
+// block b goes to float 4 (b - b0) mod RING, and a block landing in [0, EXT) also to its mirror past RING, so that a
+// run of <= EXT floats starting anywhere in the ring reads linearly.
+template <int RING = 0, int EXT = 0, typename A>
 __device__ __forceinline__ void capture_blocks(const A &a, int wave_len, float *rbase, int b0, int bs, int be, int lane,
                                                uint32_t t_lo, uint32_t t_hi, uint32_t qs, float sigma) {
     const PhiloxHead hd = philox_head(t_lo, t_hi, STREAM_NOISE | qs, a.k1);
@@ -610,7 +614,15 @@ __device__ __forceinline__ void capture_blocks(const A &a, int wave_len, float *
 #pragma unroll
         for (int u = 0; u < FRAME_CAP_U; ++u)
             if (bb + 64 * u <= be) {
-                *reinterpret_cast<float4 *>(rbase + 4 * (bb + 64 * u - b0)) = v[u];
+                if constexpr (RING > 0) {
+                    uint32_t pos = 4u * (uint32_t)(bb + 64 * u - b0);       // < 3 RING: two unsigned reductions
+                    pos = min(pos, pos - (uint32_t)RING);
+                    pos = min(pos, pos - (uint32_t)RING);
+                    *reinterpret_cast<float4 *>(rbase + pos) = v[u];
+                    if (pos < (uint32_t)EXT) *reinterpret_cast<float4 *>(rbase + pos + RING) = v[u];
+                } else {
+                    *reinterpret_cast<float4 *>(rbase + 4 * (bb + 64 * u - b0)) = v[u];
+                }
             }
     }
 }
@@ -1338,18 +1350,23 @@ void launch_frame_fix(hipStream_t st, const FrameArgs &a, dim3 grid, size_t lds)
 #elif defined(OFDM_FRAME_LONG_TU)
 // ---------------------------------------------------------------- K4b for long captures
 // Frames of 5..8 data symbols (ofdm_set_message) give captures of 4,482..5,955 samples: 18-24 KB of real parts per
-// wave, so frame_sync_kernel<0, 0> fits one four-wave block per CU (1 wave per SIMD).  This kernel keeps at most
-// LW_RES = 4,016 capture samples resident per wave (16 KB; two blocks, 2 waves per SIMD) by detecting in rounds
-// of 64 lanes x 31 positions (LW_ROUND = 1,984 positions, 2,031 samples each) and generating the capture in
-// pieces, all from the same counter-based Philox stream as the whole capture:
-//   1. samples [0, min(L, LW_RES)) -> rounds 0 and 1 (positions [0, 3,968): two frame periods);
+// wave, so frame_sync_kernel<0, 0> fits one four-wave block per CU (1 wave per SIMD).  This kernel keeps the capture
+// in a ring of LW_RING = 2,976 floats per wave (+ a 96-float mirror: 12 KB, twelve waves per CU, 3 per SIMD) that
+// always holds the last 2,973 samples generated, detects in rounds of 64 lanes x 31 positions (LW_ROUND = 1,984
+// positions, LW_PIECE = 2,031 samples each) and generates the capture a round at a time, all from the same
+// counter-based Philox stream as the whole capture:
+//   1. round 0's samples [0, 2,031) -> round 0; round 1's [1,984, 4,015) -> round 1 (two frame periods);
 //   2. lazy (as frame_sync_kernel's, one round later): Packet_Selection is decided by rounds 0 and 1 when their
 //      least valid front (its +230 check inside them) has a later front inside them: fronts and checks depend
 //      only on earlier positions, and every later front lies past it.  Then round 2 and its samples are skipped;
-//   3. otherwise samples [2 LW_ROUND, L) over the region -> round 2 (positions [3,968, Lc)) and the selection
-//      over all three rounds (a.no_lazy: always);
-//   4. when the matched filter's samples [p - 20, p + 2 (nfr - 1) + 10] are not resident (the first valid front
-//      past ~2,070, or piece 1 overwritten by step 3), they are generated again into the region.
+//      the rounds' crossing masks stay in registers, so the rule needs no samples;
+//   3. otherwise round 2's samples [3,968, L) -> round 2 and the selection over all three rounds (a.no_lazy: always);
+//   4. the matched filter's samples [p - 20, p + 2 (nfr - 1) + 10] (1,949 for 8 data symbols): the part the ring does
+//      not hold is generated (63 % of the bench's items, 0.88 capture passes per item on average).
+// Reads index the ring ((n + off) mod LW_RING): a lane's detection run (80 floats) and a matched-filter run (29) read
+// linearly through the mirror.  Round 6 A/Bs (profiles/r06/frame/ab_long12.txt, ab_ring.txt): two rounds resident
+// (16 KB per wave) in 9-wave blocks, 3, 2, 2, 2 waves on a CU's SIMDs 8.34-8.38e8; one round's piece in 12-wave blocks,
+// the whole window generated again 8.58-8.62e8; the ring 8.76-8.78e8.
 // The filtered frame fr[] then overwrites the region: a lane holds its runs' outputs in registers until every
 // lane's reads are done.  Packet detection / selection, the matched filter, CFO and hand-off are the generic
 // kernel's arithmetic, so every counter and packet_idx equals frame_sync_kernel<0, 0>'s
@@ -1358,7 +1375,8 @@ void launch_frame_fix(hipStream_t st, const FrameArgs &a, dim3 grid, size_t lds)
 // frame period, >= 1,940 positions, apart).
 constexpr int LW_CHUNK = 31;
 constexpr int LW_ROUND = 64 * LW_CHUNK;              // 1,984 positions per round
-constexpr int LW_RES = 2 * LW_ROUND + 48;             // resident capture samples (rounds 0 and 1 and their windows)
+constexpr int LW_PIECE = LW_ROUND + 47;               // a round's samples: its positions and their 47-sample windows
+constexpr int LW_RING = 2976, LW_EXT = 96;             // the capture ring (floats, a multiple of 4) and its mirror
 constexpr int LW_MAXP = 3;                            // matched-filter passes of 64 runs (33 + 13 nd <= 137 runs)
 #define FRAME_MF_B64_LONG FRAME_MF_B64_GEN   // lds_readn form of the long kernel's matched filter
 template <int W>
@@ -1404,7 +1422,17 @@ __global__ __launch_bounds__(64 * W, FRAME_LONG_MINW) void frame_sync_long_kerne
         }
         rx_start = __builtin_amdgcn_readfirstlane(rx_start);
         const int off = rx_start & 3, b0 = rx_start >> 2;
-        const float *r = rbase + off;                        // r[n] = Re capture sample n of the resident piece
+        // capture sample n lives at ring float (n + off) mod LW_RING (and its mirror past LW_RING when < LW_EXT)
+        auto ring = [&](int n) {
+            uint32_t x = (uint32_t)(n + off);
+            x = min(x, x - (uint32_t)LW_RING);
+            return (int)min(x, x - (uint32_t)LW_RING);
+        };
+        // samples [n_lo, n_hi) into the ring (whole Philox blocks: up to 3 samples either side, with their own values)
+        auto gen = [&](int n_lo, int n_hi) {
+            capture_blocks<LW_RING, LW_EXT>(a, wave_len, rbase, b0, (rx_start + n_lo) >> 2, (rx_start + n_hi - 1) >> 2, lane,
+                                            t_lo, t_hi, qs, sigma);
+        };
         const int im0 = im_mod(rx_start);
         int lx = lane;
         opaque(lx);
@@ -1413,14 +1441,14 @@ __global__ __launch_bounds__(64 * W, FRAME_LONG_MINW) void frame_sync_long_kerne
         // view of the capture (sample n at rp[n]) ----
         unsigned long long cm[3] = {0ull, 0ull, 0ull};
         int first[3] = {-1, -1, -1}, last[3] = {-1, -1, -1};
-        auto detect = [&](auto rc, const float *rp) {
+        auto detect = [&](auto rc) {
             constexpr int rho = decltype(rc)::value;
             const int n0 = rho * LW_ROUND + lx * LW_CHUNK, n1 = min(n0 + LW_CHUNK, Lc);
             unsigned long long cmask = 0ull;
             if (n0 < n1) {
                 using LdsF = const __attribute__((address_space(3))) float;
                 LdsF *ti_ = (LdsF *)(imt + im_mod(im0 + rho * LW_ROUND) + lx * LW_CHUNK);   // uniform base + lane offset
-                LdsF *tr_ = (LdsF *)(rp + n0);
+                LdsF *tr_ = (LdsF *)(rbase + ring(n0));                 // 80 floats: inside ring + mirror
                 opaque(ti_);
                 opaque(tr_);
                 float sx = 0.f, sy = 0.f, pw = 0.f;
@@ -1474,12 +1502,16 @@ __global__ __launch_bounds__(64 * W, FRAME_LONG_MINW) void frame_sync_long_kerne
             first[rho] = cmask ? n0 + __builtin_ctzll(cmask) : -1;
             last[rho] = cmask ? n0 + 63 - __builtin_clzll(cmask) : -1;
         };
-        // piece 1: samples [0, min(L, LW_RES)), rounds 0 and 1
-        const int res_end = min(L, LW_RES);
-        capture_blocks(a, wave_len, rbase, b0, b0, (rx_start + res_end - 1) >> 2, lane, t_lo, t_hi, qs, sigma);
+        // round rho's piece: samples [rho LW_ROUND, min(L, rho LW_ROUND + LW_PIECE)), the ring then holding the last
+        // LW_RING - 3 samples generated
+        auto piece = [&](int rho) { gen(rho * LW_ROUND, min(L, rho * LW_ROUND + LW_PIECE)); };
+        piece(0);
         wave_lds_sync();
-        detect(std::integral_constant<int, 0>{}, r);
-        detect(std::integral_constant<int, 1>{}, r);
+        detect(std::integral_constant<int, 0>{});
+        wave_lds_sync();                                      // round 0's loads are done: round 1's piece overwrites
+        piece(1);
+        wave_lds_sync();
+        detect(std::integral_constant<int, 1>{});
         // the crossing bit of position pos (< Lc) from the lane that owns it (ds_bpermute)
         auto crossing = [&](int pos) {
             const int rd = pos / LW_ROUND, rel = pos - rd * LW_ROUND;
@@ -1518,37 +1550,31 @@ __global__ __launch_bounds__(64 * W, FRAME_LONG_MINW) void frame_sync_long_kerne
         // lazy: rounds 0 and 1 decide when their least valid front has a later front in them (the full rule then
         // picks the same front: see the header); otherwise round 2 over the region and the selection over all rounds
         int cand = R == 3 && !a.no_lazy ? select(2, min(2 * LW_ROUND, Lc)) : 0x7fffffff;
-        bool res1 = true;                                     // piece 1 still in the region
+        int held = 1;                                         // the round whose piece the region holds
         if (cand == 0x7fffffff) {
             if (R == 3) {
-                wave_lds_sync();                              // rounds 0-1's loads are done: piece 2 overwrites
-                capture_blocks(a, wave_len, rbase, b0 + LW_ROUND / 4, (rx_start + 2 * LW_ROUND) >> 2,
-                               (rx_start + L - 1) >> 2, lane, t_lo, t_hi, qs, sigma);
+                wave_lds_sync();                              // round 1's loads are done: round 2's piece overwrites
+                piece(2);
                 wave_lds_sync();
-                detect(std::integral_constant<int, 2>{}, r - LW_ROUND);   // sample n at region float off + n - LW_ROUND
-                res1 = false;
+                detect(std::integral_constant<int, 2>{});
+                held = 2;
             }
             cand = select(R, Lc);
         }
         const bool sync_fail = cand == 0x7fffffff;
         const int p = sync_fail ? 0 : cand + 10 + 1;
-        // ---- the matched filter's samples [p - 20, p + 2 (nfr - 1) + 10]: resident, or generated again.  After
-        // piece 2 (written from block b0 + LW_ROUND / 4 on) the region still holds piece 1's samples [0, LW_ROUND - 4)
-        // at their piece-1 places and piece 2's samples [2 LW_ROUND, L) at theirs: a window inside either is read
-        // where it lies (a failed sync, p = 0, reads [0, 2 nfr - 10): the low-SNR items that need round 2) ----
-        const float *rm = r;
+        // ---- the matched filter's samples [p - 20, p + 2 (nfr - 1) + 10] (at most 1,949 < LW_RING - 6): the ring holds
+        // [res_lo, res_hi) of them after the last round's piece; the missing end of the window is generated -- forward
+        // past res_hi (evicting only samples before the window) or backward below res_lo (evicting only samples past
+        // it).  A failed sync (p = 0) reads [0, 2 nfr - 10). ----
         {
             const int lo = max(p - 20, 0), hi = min(p + 2 * (nfr - 1) + 10, L - 1);
-            const bool in1 = res1 ? hi < res_end : hi < LW_ROUND - 4;
-            const bool in2 = !res1 && lo >= 2 * LW_ROUND;
-            if (in2) rm = r - LW_ROUND;
-            if (!in1 && !in2) {
-                const int s0 = lo & ~3;
+            const int res_hi = min(L, held * LW_ROUND + LW_PIECE), res_lo = res_hi + 3 - LW_RING;
+            if (hi >= res_hi || lo < res_lo) {
                 wave_lds_sync();                              // detection's loads are done
-                capture_blocks(a, wave_len, rbase, (rx_start + s0) >> 2, (rx_start + s0) >> 2, (rx_start + hi) >> 2, lane,
-                               t_lo, t_hi, qs, sigma);
+                if (hi >= res_hi) gen(max(lo, res_hi), hi + 1);
+                else gen(lo, min(hi + 1, res_lo));
                 wave_lds_sync();
-                rm = r - s0;                                  // sample n at rbase + off + n - s0
             }
         }
         // ---- RRC matched filter at the needed instants (frame_sync_kernel's runs), outputs held in registers ----
@@ -1563,8 +1589,7 @@ __global__ __launch_bounds__(64 * W, FRAME_LONG_MINW) void frame_sync_long_kerne
 #pragma unroll
             for (int j = 0; j < 11; ++j) asm volatile("v_mov_b32 %0, %1" : "=v"(tv[j]) : "s"(tp[j]));
         }
-        const int offm = (int)(rm - rbase);                   // float offset of sample 0 in the region (may be < 0)
-        const int par_r = (offm + p) & 1, par_i = (im0 + p) & 1;
+        const int par_r = (off + p) & 1, par_i = (im0 + p) & 1;    // ring floats keep the parity (LW_RING even)
         constexpr int MF_RUN = 5, MF_W = 2 * MF_RUN + 19;
         constexpr int c0r = (32 + MF_RUN - 1) / MF_RUN, c1r = c0r + (128 + MF_RUN - 1) / MF_RUN;
         constexpr int cd = (64 + MF_RUN - 1) / MF_RUN;
@@ -1593,7 +1618,8 @@ __global__ __launch_bounds__(64 * W, FRAME_LONG_MINW) void frame_sync_long_kerne
             if (u < n_runs && n_lo >= 0 && p + 2 * (e - 1) < L) {
                 float xr[MF_W], xi[MF_W];
                 const int si = im_mf + 2 * s0;                                // < 3 periods: inside the copies
-                if (par_r) lds_readn<1, FRAME_MF_B64_LONG>(rm, n_lo, xr); else lds_readn<0, FRAME_MF_B64_LONG>(rm, n_lo, xr);
+                const int rl = ring(n_lo);                                    // 29 floats: inside ring + mirror
+                if (par_r) lds_readn<1, FRAME_MF_B64_LONG>(rbase, rl, xr); else lds_readn<0, FRAME_MF_B64_LONG>(rbase, rl, xr);
                 if (par_i) lds_readn<1, FRAME_MF_B64_LONG>(imt, si, xi); else lds_readn<0, FRAME_MF_B64_LONG>(imt, si, xi);
 #pragma unroll
                 for (int o = 0; o < MF_RUN; ++o) {
@@ -1618,7 +1644,7 @@ __global__ __launch_bounds__(64 * W, FRAME_LONG_MINW) void frame_sync_long_kerne
                                 const int m = n - tt;
                                 const int mc = min(max(m, 0), L - 1);
                                 const bool in = m >= 0 && m < L;
-                                const float xr = in ? rm[mc] : 0.f, xi = in ? imt[im_mod(im0 + mc)] : 0.f;
+                                const float xr = in ? rbase[ring(mc)] : 0.f, xi = in ? imt[im_mod(im0 + mc)] : 0.f;
                                 const float h = tv[tt <= 10 ? tt : 20 - tt];
                                 v.x = fmaf(xr, h, v.x);
                                 v.y = fmaf(xi, h, v.y);
@@ -1706,12 +1732,11 @@ const void *frame_fix_kernel();                                         // ofdm_
 void launch_frame_fix(hipStream_t st, const FrameArgs &a, dim3 grid, size_t lds);
 const void *frame_long_kernel();                                        // ofdm_frame_long.hip
 void launch_frame_long(hipStream_t st, const FrameArgs &a, dim3 grid, size_t lds);
-// the long-capture kernel's per-wave region (floats): the resident piece (LW_RES samples + capture offset + the last
-// detection lane's block overshoot), which also holds a regenerated matched-filter window and then fr[]
-constexpr int FRAME_LONG_REGION = 4032;
+// the long-capture kernel's per-wave region (floats): the capture ring and its mirror, then fr[]
+constexpr int FRAME_LONG_REGION = 3072;                // LW_RING + LW_EXT
 // the long kernel's imaginary-part table runs LONG_TABLE_REACH floats past one period: a detection round's lanes
 // read up to 63 x 31 + 5 x 16 = 2,033 floats past its base, a matched-filter pass up to 2 x 956 + 29 = 1,941
-// (8 data symbols).  8-symbol frames: 2 blocks x (256 + 15,952 + 4 x 16,128 B) = 161.4 KB of the CU's 160 KiB
+// (8 data symbols).  8-symbol frames: 256 + 15,952 + 12 x 12,288 B = 163,664 B of the CU's 163,840
 constexpr int LONG_TABLE_REACH = 2048;
 constexpr int FRAME_LONG_MIN_CAP = 4100;     // captures longer than this (frames of >= 5 data symbols) run it
 
@@ -1860,8 +1885,8 @@ static int run_frame_chunk(Ctx *c, FrameArgs &a) {
     // statistics) runs the instantiation with that geometry folded in; OFDM_FRAME_GENERIC=1 forces the generic
     // one (the equivalence test)
     const int64_t runs = (a.n_items + FRAME_ITEM_RUN - 1) / FRAME_ITEM_RUN;
-    // long captures (frames of >= 5 data symbols): frame_sync_long_kernel keeps two capture pieces per wave, not
-    // the whole capture (2 waves per SIMD instead of 1); sweeps only.  OFDM_FRAME_NO_LONG=1 forces the generic kernel
+    // long captures (frames of >= 5 data symbols): frame_sync_long_kernel keeps one detection round's piece per wave, not
+    // the whole capture (3 waves per SIMD instead of 1); sweeps only.  OFDM_FRAME_NO_LONG=1 forces the generic kernel
     // (the equivalence test)
     const bool is_long = a.cap_len > FRAME_LONG_MIN_CAP && a.cap_len - 47 <= 3 * 64 * 31 && !a.ext && !a.dbg_res &&
                          !a.dbg_ints && !a.dbg_bits && !a.dbg_eq && !a.dbg_corr && !a.dbg_frame && !a.word_stats &&

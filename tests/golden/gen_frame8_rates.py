@@ -7,9 +7,11 @@ the same bits as the GPU's ofdm_set_message) with real-only AWGN at sigma^2 = P_
 frame-mode noise, ofdm_frame.hip): Packet_Detection's M (OFDM.c:659-683, tests/test_lazy_rule.corr_out) and the
 kernel's decisions --
   decided   rounds 0-1 (positions [0, 2 x 1,984)) decide Packet_Selection (the lazy round-2 skip);
-  regen     the matched filter's window [p - 20, p + 2 (nfr - 1) + 10] is generated again: decided items whose window
-            ends past the resident piece (4,016 samples), undecided ones whose window is in neither the first 1,980
-            samples nor [3,968, L) (ofdm_frame.hip, the long kernel's residency rule);
+  regen     the matched filter's window [p - 20, p + 2 (nfr - 1) + 10] is not all in the capture ring after the last
+            detection round's piece (ofdm_frame.hip, the long kernel's residency rule: the ring holds the last
+            LW_RING - 3 = 2,973 samples generated, [1,042, 4,015) for decided items, [L - 2,973, L) for undecided ones),
+            so its missing end is generated; regen_passes: the capture passes (256 Philox blocks each) that takes;
+            regen_fwd / regen_fwd_passes: the same for the items whose window's END is generated (past the ring)
   sync_fail no packet selected (p = 0).
 The rates are statistical (double precision here, fp32 sums on the GPU: a capture at the 0.75 threshold may fall
 either way), so the fixture carries its sample size.
@@ -31,6 +33,7 @@ sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "tests"))
 
 LW_ROUND = 64 * 31
+LW_RING = 2976
 LEN_RRC_RX = 10
 SNR_GRID = np.arange(0.0, 31.0, 2.0)
 
@@ -54,10 +57,9 @@ def rates(wave: np.ndarray, snr_db: float, n: int, seed: int) -> dict:
     L = int(0.307 * len(wave))
     Lc = L - 47
     nfr = 320 + 80 * 8
-    res_end = min(L, 2 * LW_ROUND + 48)
     sigma = np.sqrt(np.mean(np.abs(wave) ** 2) / 10 ** (snr_db / 10))
     rng = np.random.default_rng(seed)
-    dec = regen = fail = 0
+    dec = regen = fail = passes = nf = pf = 0
     for _ in range(n):
         s = int(rng.integers(0, len(wave) - L))
         cap = wave[s:s + L] + sigma * rng.standard_normal(L)       # real-only AWGN (D7)
@@ -67,12 +69,21 @@ def rates(wave: np.ndarray, snr_db: float, n: int, seed: int) -> dict:
             ok, p = selection(m, Lc)
             p = p if ok else 0
         lo, hi = max(p - 20, 0), min(p + 2 * (nfr - 1) + 10, L - 1)
-        in1 = hi < res_end if d else hi < LW_ROUND - 4
-        in2 = (not d) and lo >= 2 * LW_ROUND
+        held = 1 if d else 2
+        res_hi = min(L, held * LW_ROUND + LW_ROUND + 47)
+        res_lo = res_hi + 3 - LW_RING
         dec += d
-        regen += not (in1 or in2)
+        if hi >= res_hi or lo < res_lo:
+            fwd = hi >= res_hi                                      # the window's end is generated, else its start
+            g0, g1 = (max(lo, res_hi), hi + 1) if fwd else (lo, min(hi + 1, res_lo))
+            blocks = ((s + g1 - 1) >> 2) - ((s + g0) >> 2) + 1      # the capture start s is the kernel's rx_start
+            regen += 1
+            passes += -(-blocks // 256)
+            nf += fwd
+            pf += -(-blocks // 256) if fwd else 0
         fail += p == 0
-    return {"snr_db": snr_db, "captures": n, "decided": dec / n, "regen": regen / n, "sync_fail": fail / n}
+    return {"snr_db": snr_db, "captures": n, "decided": dec / n, "regen": regen / n, "regen_passes": passes / n,
+            "regen_fwd": nf / n, "regen_fwd_passes": pf / n, "sync_fail": fail / n}
 
 
 def main(argv=None):
@@ -90,7 +101,8 @@ def main(argv=None):
     out = {"generator": f"tests/golden/gen_frame8_rates.py --captures {a.captures}",
            "message": bench.FRAME8_MESSAGE.decode(), "capture_len": int(0.307 * len(wave)),
            "rows": rows,
-           "grid_mean": {k: float(np.mean([r[k] for r in rows])) for k in ("decided", "regen", "sync_fail")}}
+           "grid_mean": {k: float(np.mean([r[k] for r in rows])) for k in ("decided", "regen", "regen_passes", "regen_fwd",
+                                                                     "regen_fwd_passes", "sync_fail")}}
     (HERE / "frame8_path_rates.json").write_text(json.dumps(out, indent=1) + "\n")
     print(json.dumps(out["grid_mean"]))
 

@@ -3,21 +3,21 @@
 item 3: every VALU instruction of the long kernel's gfx950 code classified (tools/isa_mix.py classes and costs) and
 weighted by how often a (trial, SNR) item executes it.
 
-usage: python tools/frame8_mix.py <pmc dir>... [--items N] [--waves 3,2,2,2] [--record]
+usage: python tools/frame8_mix.py <pmc dir>... [--items N] [--waves 3,3,3,3] [--record]
 
 frame_mix.py (the reference frame's sync kernel) finds its phases by code patterns; the long kernel's 1,500 blocks
-(three capture call sites, three detection rounds, unrolled matched-filter passes with their per-instant fallbacks)
+(four capture call sites, three detection rounds, unrolled matched-filter passes with their per-instant fallbacks)
 are attributed by their SOURCE instead.  The library's TU is compiled once more with -g (same flags; the
 instruction stream differs from the product build by a few instructions, printed as `g_build_instr_delta`), and
 each instruction is mapped to the kernel-body statement it comes from: the DW_AT_call_line of the outermost
 inlined call holding it (capture_blocks, the detect / select lambdas, ...), else its own line.  Weights per item:
   * outside the item loop: 0;
-  * the undecided path (`if (cand == 0x7fffffff)`: piece 2, detection round 2, the selection over three rounds): u;
-  * the matched-filter window generated again (`if (!in1 && !in2)`): g;
+  * the undecided path (`if (cand == 0x7fffffff)`: round 2's piece and detection, the selection over three rounds): u;
+  * the matched-filter window's missing end generated (the capture ring does not hold all of it): g;
   * the per-instant matched-filter path (windows leaving the capture): 0, its per-pass skeleton 1/3 (pass 2's
     lanes past the 137 runs take it);
-  * a capture call site's pass loop: its passes per item (piece 1: 1,004 Philox blocks / 256 per pass = 4; piece 2
-    and the regenerated window: 2), times the call site's weight;
+  * a capture call site's pass loop: piece(0), piece(1), piece(2) 2 passes per item (a round's 2,031 samples: <= 509
+    Philox blocks, 256 per pass), times the call site's weight; the window's missing end: the fixture's passes per item;
   * the hand-off loop: 1 + n_data = 9 iterations;
   * every other instruction of the item loop: 1.
 g is the fraction tests/golden/frame8_path_rates.json records for the bench grid (a CPU simulation of the kernel's
@@ -50,7 +50,7 @@ sys.path.insert(0, str(PKG))
 from isa_mix import COST, classify  # noqa: E402
 import frame_mix  # noqa: E402
 
-LONG = "_ZN4ofdm22frame_sync_long_kernelILi9EEEvNS_9FrameArgsE"
+LONG = "_ZN4ofdm22frame_sync_long_kernelILi12EEEvNS_9FrameArgsE"
 SYM = "_ZN4ofdm16frame_sym_kernelILb0ELi0EEEvNS_9FrameArgsE"
 CLASSES = ("fast", "slow", "trans", "cnd")
 LLVM = Path("/opt/rocm/lib/llvm/bin")
@@ -145,20 +145,22 @@ def anchors() -> dict:
     k = src_line(t, "void frame_sync_long_kernel(FrameArgs a)") - 1
     a = {"kernel": k + 1,
          "item_for": src_line(t, "for (int64_t i = run_end - FRAME_ITEM_RUN; i < a.n_items;) {", k),
-         "piece1": src_line(t, "capture_blocks(a, wave_len, rbase, b0, b0,", k),
+         "piece0": src_line(t, "piece(0);", k),
+         "piece1": src_line(t, "piece(1);", k),
          "undec_lo": src_line(t, "if (cand == 0x7fffffff) {", k),
          "undec_hi": src_line(t, "const bool sync_fail = cand == 0x7fffffff;", k),
-         "regen_lo": src_line(t, "if (!in1 && !in2) {", k),
+         "regen_lo": src_line(t, "if (hi >= res_hi || lo < res_lo) {", k),
          "fb_lo": src_line(t, "// the per-instant path (windows leaving the capture)", k),
          "fb_inner_lo": src_line(t, "if (n >= L + 20) {", k),
          "handoff_lo": src_line(t, "for (int j = lx; j < 64 * nw; j += 64) {", k),
          "handoff_hi": src_line(t, "dst[win_off(n, a.ipb, nw) + w] = v;", k)}
-    a["regen_hi"] = src_line(t, "rm = r - s0;", a["regen_lo"] - 1)
+    a["regen_hi"] = src_line(t, "else gen(lo, min(hi + 1, res_lo));", a["regen_lo"] - 1)
     a["fb_inner_hi"] = src_line(t, "v.y = fmaf(xi, h, v.y);", a["fb_inner_lo"] - 1)
     a["fb_hi"] = src_line(t, "mfo[pi][o] = v;", a["fb_inner_hi"] - 1)
     a["item_end"] = src_line(t, "// the next capture overwrites this item's region", a["handoff_hi"] - 1)
-    a["undec_capture"] = src_line(t, "capture_blocks(", a["undec_lo"] - 1)
-    a["regen_capture"] = src_line(t, "capture_blocks(", a["regen_lo"] - 1)
+    a["undec_capture"] = src_line(t, "piece(2);", a["undec_lo"] - 1)
+    a["regen_fwd"] = src_line(t, "if (hi >= res_hi) gen(max(lo, res_hi), hi + 1);", a["regen_lo"] - 1)
+    a["regen_bwd"] = a["regen_hi"]
     return a
 
 
@@ -207,8 +209,12 @@ def chains(ins, sites, rows) -> dict:
     return out
 
 
-def weights(ins, sites, rows, a, g: float, nw: int):
-    """per-instruction weight as (constant, coefficient of u) -- g enters the constant"""
+def weights(ins, sites, rows, a, rates: dict, nw: int):
+    """per-instruction weight as (constant, coefficient of u) -- the fixture's regeneration rates enter the constant:
+    items generating the end of their matched-filter window (forward) or its start (backward), and their passes"""
+    g = rates["regen"]
+    gf, gb = rates["regen_fwd"], rates["regen"] - rates["regen_fwd"]
+    pf, pb = rates["regen_fwd_passes"], rates["regen_passes"] - rates["regen_fwd_passes"]
     ch = chains(ins, sites, rows)
     lp = loops(ins)
     item = max(lp, key=lambda l: l[1] - l[0])
@@ -230,6 +236,10 @@ def weights(ins, sites, rows, a, g: float, nw: int):
         c, cu = 1.0, 0.0
         if within(c_, a["undec_lo"], a["undec_hi"] - 1):
             c, cu = 0.0, 1.0
+        elif within(c_, a["regen_fwd"], a["regen_fwd"]):
+            c = gf
+        elif within(c_, a["regen_bwd"], a["regen_bwd"]):
+            c = gb
         elif within(c_, a["regen_lo"], a["regen_hi"] + 1):
             c = g
         elif within(c_, a["fb_inner_lo"], a["fb_inner_hi"] + 2):
@@ -238,8 +248,12 @@ def weights(ins, sites, rows, a, g: float, nw: int):
             c = 1.0 / 3.0
         mult = 1.0
         if any(l[0] <= addr <= l[1] for l in phil):
-            site = next((x for x in c_ if x in (a["piece1"], a["undec_capture"], a["regen_capture"])), None)
-            mult = {a["piece1"]: 4.0, a["undec_capture"]: 2.0, a["regen_capture"]: 2.0}.get(site, 1.0)
+            sites_ = (a["piece0"], a["piece1"], a["undec_capture"], a["regen_fwd"], a["regen_bwd"])
+            site = next((x for x in c_ if x in sites_), None)
+            # a round's piece: 2,031 samples, <= 509 Philox blocks = 2 passes of 256; the window's missing end: gp passes
+            # per item over the g items that generate it
+            mult = (1.0 if site is None else (pf / gf if gf else 0.0) if site == a["regen_fwd"]
+                    else (pb / gb if gb else 0.0) if site == a["regen_bwd"] else 2.0)
         elif within(c_, a["handoff_lo"], a["handoff_hi"]) and any(l[0] <= addr <= l[1] for l in inner_loops):
             mult = float(nw)
         w[addr] = (c * mult, cu * mult)
@@ -257,7 +271,7 @@ def tally(ins, w):
     return cls
 
 
-def model(dirs, items: float, waves="3,2,2,2") -> dict:
+def model(dirs, items: float, waves="3,3,3,3") -> dict:
     rates = json.loads((ROOT / "tests" / "golden" / "frame8_path_rates.json").read_text())
     g, u_sim = rates["grid_mean"]["regen"], 1.0 - rates["grid_mean"]["decided"]
     a = anchors()
@@ -268,7 +282,7 @@ def model(dirs, items: float, waves="3,2,2,2") -> dict:
         n_plain = len(disasm(on, LONG))
         sites = inline_sites(og, ins[0][0])
         rows = line_table(og)
-    w, item, phil = weights(ins, sites, rows, a, g, 9)
+    w, item, phil = weights(ins, sites, rows, a, rates["grid_mean"], 9)
     ms, my = frame_mix.pmc(dirs, "frame_sync_long_kernel"), frame_mix.pmc(dirs, "frame_sym_kernel")
     meas = {k: ms[c] / items for k, c in frame_mix.MEAS.items()}
     v = ms["SQ_INSTS_VALU"] / items
@@ -299,8 +313,9 @@ def model(dirs, items: float, waves="3,2,2,2") -> dict:
     ycls, _, _ = frame_mix.tally(ybb, {i: (1.0, 0.0) for i, b in enumerate(ybb) if b[1] >= 1})
     vy = my["SQ_INSTS_VALU"] / items
     ny = {k: vy * ycls[k][0] / ycls["valu"][0] for k in CLASSES}
-    # waves: the sync kernel's waves on each of a CU's four SIMDs (9-wave blocks, one per CU: 3, 2, 2, 2).  Items are
-    # handed out dynamically, so the chip's cap is the mean of the SIMDs' caps; the symbol kernel runs 2 per SIMD
+    # waves: the sync kernel's waves on each of a CU's four SIMDs (12-wave blocks, one per CU: 3 each; the 9-wave build
+    # ran 3, 2, 2, 2).  Items are handed out dynamically, so the chip's cap is the mean of the SIMDs' caps; the symbol
+    # kernel runs 2 per SIMD
     simds = [int(x) for x in str(waves).split(",")]
     cyc_y = sum(COST[2][k] * ny[k] for k in CLASSES)
     cyc_by = {w: sum(COST[w][k] * n[k] for k in CLASSES) for w in set(simds)}
@@ -328,7 +343,7 @@ def model(dirs, items: float, waves="3,2,2,2") -> dict:
 
 def main(argv):
     dirs = [x for x in argv if not x.startswith("--") and Path(x).is_dir()]
-    waves = argv[argv.index("--waves") + 1] if "--waves" in argv else "3,2,2,2"
+    waves = argv[argv.index("--waves") + 1] if "--waves" in argv else "3,3,3,3"
     summary_p = ROOT / "profiles" / "pmc_summary.json"
     if "--items" in argv:
         items = float(argv[argv.index("--items") + 1])
