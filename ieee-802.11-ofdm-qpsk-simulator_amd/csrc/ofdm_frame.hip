@@ -1262,7 +1262,10 @@ __global__ __launch_bounds__(SYM_THREADS, FRAME_SYM_MINB) void frame_sym_kernel(
             part_a[quad][sl] = dlane ? st.ax : 0u;
         }
         if (DUMP && dump && a.dbg_bits) { a.dbg_bits[3 * dsym] = st.d[0]; a.dbg_bits[3 * dsym + 1] = st.d[1]; a.dbg_bits[3 * dsym + 2] = st.d[2]; }
-        __syncthreads();
+        // an item's quads are in one wave when it has one quad (FIX_ND = 2): its totals need a wave's sync, not the
+        // block's (round 6 A/B, profiles/r06/frame/ab_symws.txt: frame +0.5 %; an L2 warm-up of the block's next tile,
+        // ab_sym.txt: -3 %)
+        if constexpr (FIX_ND > 0 && FIX_ND <= 2) wave_lds_sync(); else __syncthreads();
         if (item_ok && qi == 0 && role == 0) {
             // the item's totals in symbol order (deterministic), then the trial's metrics
             float fe = 0.f;
@@ -1290,8 +1293,9 @@ __global__ __launch_bounds__(SYM_THREADS, FRAME_SYM_MINB) void frame_sym_kernel(
             }
             if (DUMP && g == 0 && a.dbg_res) { a.dbg_res[0] = db; a.dbg_res[1] = dbp; a.dbg_res[2] = (float)ferr / (96.0f * n_data); }
         }
-        __syncthreads();
+        if constexpr (FIX_ND > 0 && FIX_ND <= 2) wave_lds_sync(); else __syncthreads();
     }
+    if constexpr (FIX_ND > 0 && FIX_ND <= 2) __syncthreads();     // every wave's counter adds are in before the flush
     for (int k = threadIdx.x; k < a.n_snr * 6; k += SYM_THREADS) {
         const int q = k / 6, s2 = k % 6;
         const int slot = s2 < 3 ? s2 : s2 + 1;           // 0 bit_err, 1 frame_err, 2 axis, 4 finite, 5 pre, 6 dbpre, 7 dbpost
