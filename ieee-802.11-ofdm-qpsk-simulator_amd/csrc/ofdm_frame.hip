@@ -1195,9 +1195,10 @@ __global__ __launch_bounds__(64 * W, FRAME_SYNC_MINW) void frame_sync_kernel(Fra
 // item (sym_quads), from which the kernel derives it back as max(2, ceil(n_data / quads)): for 4 data symbols that
 // is 2 quads of {LTF, LTF, D, D}, the same 8 lanes as {LTF, D, D, D} would take.
 template <bool DUMP, int FIX_ND>   // DUMP: item 0's bits / subcarriers / metrics for ofdm_receiver
-#define FRAME_SYM_MINB 2   // 3 waves/SIMD spills 196 VGPRs: frame mode 9 % slower
+#define FRAME_SYM_MINB 2   // the parity-dump instance (256 VGPRs); the sweep instances run 3 waves/SIMD (<= 168 VGPRs,
+                           // no spills: round 6 A/B, profiles/r06/frame/ab_sym3.txt, frame8 +1.2 %, frame +0.5 %)
 // FIX_ND > 0: n_data as a compile-time constant (the reference message's sweep: the hand-off offsets fold)
-__global__ __launch_bounds__(SYM_THREADS, FRAME_SYM_MINB) void frame_sym_kernel(FrameArgs a) {
+__global__ __launch_bounds__(SYM_THREADS, DUMP ? FRAME_SYM_MINB : 3) void frame_sym_kernel(FrameArgs a) {
     const int n_data = FIX_ND ? FIX_ND : a.n_data;
     __shared__ unsigned long long acc[OFDM_MAX_SNR][8];
     constexpr int DPQ_MAX = FIX_ND ? 2 : 3;
@@ -1209,8 +1210,9 @@ __global__ __launch_bounds__(SYM_THREADS, FRAME_SYM_MINB) void frame_sym_kernel(
     // quads per item and data lanes per quad: 2 with FIX_ND, else from the tile size (sym_quads)
     const int qpi = FIX_ND ? (FIX_ND + 1) / 2 : (SYM_THREADS / 4) / a.ipb;
     const int dpq = FIX_ND ? 2 : max(2, (n_data + qpi - 1) / qpi), r0 = 4 - dpq;   // first data role
-    const int ipb = (SYM_THREADS / 4) / qpi;                                // items per block
-    const int item_l = quad / qpi, qi = quad - item_l * qpi;
+    // items never straddle a wave: a wave's 16 quads carry 16 / qpi whole items (qpi = 3: 5 items, one idle quad)
+    const int ipw = 16 / qpi, ipb = 4 * ipw;                               // items per wave, per block
+    const int wq = quad & 15, item_l = (quad >> 4) * ipw + wq / qpi, qi = wq - (wq / qpi) * qpi;
     const int dsym = dpq == 2 ? 2 * qi + (role & 1) : 3 * qi + max(role - 1, 0);
     const int nw = 1 + n_data;
     const int dsc = min(dsym, n_data - 1);
@@ -1219,7 +1221,7 @@ __global__ __launch_bounds__(SYM_THREADS, FRAME_SYM_MINB) void frame_sym_kernel(
     const int w = role < r0 ? 0 : 1 + dsc;
     for (int64_t base = (int64_t)blockIdx.x * ipb; base < a.n_items; base += (int64_t)gridDim.x * ipb) {
         const int64_t i = base + item_l;
-        const bool item_ok = item_l < ipb && i < a.n_items;
+        const bool item_ok = wq < ipw * qpi && i < a.n_items;
         const bool dlane = item_ok && role >= r0 && dsym < n_data;
         const float2 *src = win_item(a.win, ipb, nw, item_ok ? i : base) + w;
         float2 x[64];
@@ -1262,10 +1264,10 @@ __global__ __launch_bounds__(SYM_THREADS, FRAME_SYM_MINB) void frame_sym_kernel(
             part_a[quad][sl] = dlane ? st.ax : 0u;
         }
         if (DUMP && dump && a.dbg_bits) { a.dbg_bits[3 * dsym] = st.d[0]; a.dbg_bits[3 * dsym + 1] = st.d[1]; a.dbg_bits[3 * dsym + 2] = st.d[2]; }
-        // an item's quads are in one wave when it has one quad (FIX_ND = 2): its totals need a wave's sync, not the
-        // block's (round 6 A/B, profiles/r06/frame/ab_symws.txt: frame +0.5 %; an L2 warm-up of the block's next tile,
-        // ab_sym.txt: -3 %)
-        if constexpr (FIX_ND > 0 && FIX_ND <= 2) wave_lds_sync(); else __syncthreads();
+        // an item's quads are in one wave (ipw whole items per wave), so its totals need a wave's sync, not the block's
+        // (round 6 A/Bs: profiles/r06/frame/ab_symws.txt, frame +0.5 %; ab_sym3.txt, with whole items per wave for
+        // 3-quad items, frame8 +0.5 % over 3 waves/SIMD alone; an L2 warm-up of the block's next tile, ab_sym.txt: -3 %)
+        if constexpr (!DUMP) wave_lds_sync(); else __syncthreads();
         if (item_ok && qi == 0 && role == 0) {
             // the item's totals in symbol order (deterministic), then the trial's metrics
             float fe = 0.f;
@@ -1293,9 +1295,9 @@ __global__ __launch_bounds__(SYM_THREADS, FRAME_SYM_MINB) void frame_sym_kernel(
             }
             if (DUMP && g == 0 && a.dbg_res) { a.dbg_res[0] = db; a.dbg_res[1] = dbp; a.dbg_res[2] = (float)ferr / (96.0f * n_data); }
         }
-        if constexpr (FIX_ND > 0 && FIX_ND <= 2) wave_lds_sync(); else __syncthreads();
+        if constexpr (!DUMP) wave_lds_sync(); else __syncthreads();
     }
-    if constexpr (FIX_ND > 0 && FIX_ND <= 2) __syncthreads();     // every wave's counter adds are in before the flush
+    if constexpr (!DUMP) __syncthreads();     // every wave's counter adds are in before the flush
     for (int k = threadIdx.x; k < a.n_snr * 6; k += SYM_THREADS) {
         const int q = k / 6, s2 = k % 6;
         const int slot = s2 < 3 ? s2 : s2 + 1;           // 0 bit_err, 1 frame_err, 2 axis, 4 finite, 5 pre, 6 dbpre, 7 dbpost
@@ -1867,7 +1869,7 @@ static int run_frame_chunk(Ctx *c, FrameArgs &a) {
     a.trial0 = a.item0 / a.n_snr;
     a.q0 = (int32_t)(a.item0 % a.n_snr);
     a.snr_magic = 0xFFFFFFFFu / (uint32_t)a.n_snr;
-    a.ipb = (SYM_THREADS / 4) / sym_quads(a.n_data);
+    a.ipb = 4 * (16 / sym_quads(a.n_data));             // whole items per wave (frame_sym_kernel)
     const size_t wbytes = (size_t)((a.n_items + a.ipb - 1) / a.ipb) * a.ipb * nw * 64 * sizeof(float2);
     int rc = c->ensure(&c->d_scratch, &c->cap_scratch, wbytes + (size_t)a.n_items * sizeof(int4) + 256);
     if (rc) return rc;

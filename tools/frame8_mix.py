@@ -315,9 +315,9 @@ def model(dirs, items: float, waves="3,3,3,3") -> dict:
     ny = {k: vy * ycls[k][0] / ycls["valu"][0] for k in CLASSES}
     # waves: the sync kernel's waves on each of a CU's four SIMDs (12-wave blocks, one per CU: 3 each; the 9-wave build
     # ran 3, 2, 2, 2).  Items are handed out dynamically, so the chip's cap is the mean of the SIMDs' caps; the symbol
-    # kernel runs 2 per SIMD
+    # kernel runs 3 per SIMD
     simds = [int(x) for x in str(waves).split(",")]
-    cyc_y = sum(COST[2][k] * ny[k] for k in CLASSES)
+    cyc_y = sum(COST[3][k] * ny[k] for k in CLASSES)          # the symbol kernel: 3 waves/SIMD since round 6
     cyc_by = {w: sum(COST[w][k] * n[k] for k in CLASSES) for w in set(simds)}
     cyc_s = sum(cyc_by[w] for w in simds) / len(simds)
     cap_s = sum(2 * v / cyc_by[w] for w in simds) / len(simds)
