@@ -185,9 +185,9 @@ def test_long_message_one_wave_blocks_equal_four_wave_blocks(pkg, monkeypatch):
 
 @pytest.mark.parametrize("msg_len", [96, 80, 49])
 def test_long_capture_kernel_equals_generic(pkg, monkeypatch, msg_len):
-    """Frames of >= 5 data symbols (captures > 4,100 samples) run frame_sync_long_kernel: two resident capture
-    pieces per wave (the last detection round's samples, then [0, 4,016)), the matched-filter window generated again
-    when it leaves the resident piece, fr[] over the region.  Every counter and packet_idx equals the generic
+    """Frames of >= 5 data symbols (captures > 4,100 samples) run frame_sync_long_kernel: the capture in a per-wave
+    ring of 2,976 floats (+ mirror) generated a detection round at a time, the part of the matched-filter window the
+    ring does not hold generated again, fr[] over the region.  Every counter and packet_idx equals the generic
     kernel's (OFDM_FRAME_NO_LONG=1), over the bench's SNR grid, for 8-, 7- and 5-symbol messages.  Every long capture
     has three detection rounds (its Lc > 2 x 1,984 positions); the 5-symbol 4,482-sample capture's last round is only
     467 positions long.  Chunked long sweeps (chunk starts off the SNR grid) are
