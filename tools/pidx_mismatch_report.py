@@ -6,6 +6,7 @@ the mismatches and how many of them the threshold explains, as one JSON object.
 
 usage (GPU box): python tools/pidx_mismatch_report.py [--wide N] > profiles/r06/pidx_mismatches.json
   --wide N: also the reference message over the bench grid (0..30 dB step 2), N trials per point
+  --wide8 N: also bench.py's frame8 message (8 data symbols, frame_sync_long_kernel) over the same grid
 """
 import json
 import sys
@@ -48,6 +49,10 @@ def main():
         if "--wide" in sys.argv:
             n = int(sys.argv[sys.argv.index("--wide") + 1])
             out.append(case(e, oracle, pkg, abi, ref_msg, [float(x) for x in range(0, 31, 2)], n))
+        if "--wide8" in sys.argv:
+            from bench import FRAME8_MESSAGE  # noqa: PLC0415
+            n = int(sys.argv[sys.argv.index("--wide8") + 1])
+            out.append(case(e, oracle, pkg, abi, FRAME8_MESSAGE, [float(x) for x in range(0, 31, 2)], n))
     oracle.set_message(ref_msg)
     print(json.dumps({"generator": "tools/pidx_mismatch_report.py", "cases": out,
                       "total_trials": sum(c["trials"] for c in out),
