@@ -558,12 +558,15 @@ __device__ __forceinline__ void lds_readn(const float *p, int s, float (&x)[N]) 
 }
 
 
+#define FRAME_CAP_U 4   // Philox blocks per lane per pass: the lazy capture's 8 + 4 blocks in passes of 4 (A/B: +1.3 % over 6, = 8)
 // Capture Philox blocks bs..be (block b = waveform samples 4b..4b+3; b0 = the capture's first block) into the
 // wave's region: the real parts of the clean waveform plus real AWGN (OFDM.c:622-655, D7).
 // RING > 0 (frame_sync_long_kernel): the region is a ring of RING floats (a multiple of 4) plus EXT mirrored floats --
 // block b goes to float 4 (b - b0) mod RING, and a block landing in [0, EXT) also to its mirror past RING, so that a
-// run of <= EXT floats starting anywhere in the ring reads linearly.
-template <int RING = 0, int EXT = 0, typename A>
+// run of <= EXT floats starting anywhere in the ring reads linearly.  Its last pass draws only ceil(rest / 64) blocks
+// per lane (the matched-filter window's missing ends are 1..483 blocks long; the detection rounds' pieces fill whole
+// passes either way).
+template <int RING = 0, int EXT = 0, bool TRIM = false, typename A>
 __device__ __forceinline__ void capture_blocks(const A &a, int wave_len, float *rbase, int b0, int bs, int be, int lane,
                                                uint32_t t_lo, uint32_t t_hi, uint32_t qs, float sigma) {
     const PhiloxHead hd = philox_head(t_lo, t_hi, STREAM_NOISE | qs, a.k1);
@@ -580,15 +583,16 @@ __device__ __forceinline__ void capture_blocks(const A &a, int wave_len, float *
     const uint32_t pb = (uint32_t)(wave_len / (4 * FR_REPS)), nb_wave = (uint32_t)(wave_len / 4);
     uint32_t bm = (uint32_t)(bs + lane) % pb;
     const bool real = a.noise == OFDM_NOISE_REAL;        // real-only AWGN (D7), or noiseless
-#define FRAME_CAP_U 4   // Philox blocks per lane per pass: the lazy capture's 8 + 4 blocks in passes of 4 (A/B: +1.3 % over 6, = 8)
-    // Passes are uniform over the wave and free of per-lane control flow: every lane loads, draws and combines
-    // its FRAME_CAP_U blocks (a lane past `be` computes a block it does not store), so the blocks' Philox rounds
-    // and Box-Muller transcendentals interleave (ILP 2 FRAME_CAP_U in the multiply chains)
-    for (int p0 = bs; p0 <= be; p0 += FRAME_CAP_U * 64) {
+    // One pass: lane l draws blocks p0 + l + 64 u, u < U, and stores those <= be.  Uniform over the wave and free of
+    // per-lane control flow: every lane loads, draws and combines its U blocks (a lane past `be` computes a block it
+    // does not store), so the blocks' Philox rounds and Box-Muller transcendentals interleave (ILP 2 U in the multiply
+    // chains).  bm advances by 64 per block drawn.
+    auto pass = [&](auto uc, int p0) {
+        constexpr int U = decltype(uc)::value;
         const int bb = p0 + lane;
-        float4 v[FRAME_CAP_U];
+        float4 v[U];
 #pragma unroll
-        for (int u = 0; u < FRAME_CAP_U; ++u) {
+        for (int u = 0; u < U; ++u) {
             const int b = bb + 64 * u;
             // the block's 4 clean real parts in one 16-B load (bm < pb: inside the table; the compiler keeps it under
             // `in`, and forcing it on every lane measured 1 % slower, profiles/r04/ab/ab_ab_ntu.txt)
@@ -598,13 +602,13 @@ __device__ __forceinline__ void capture_blocks(const A &a, int wave_len, float *
             bm = bm + 64 >= pb ? bm + 64 - pb : bm + 64;           // (bm + 64) mod pb (pb > 64)
         }
         if (real) {         // sigma z = sqrt(K log2 u1) (cos | sin 2 pi u2) per pair
-            uint32_t c2[FRAME_CAP_U];
-            uint4 o[FRAME_CAP_U];
+            uint32_t c2[U];
+            uint4 o[U];
 #pragma unroll
-            for (int u = 0; u < FRAME_CAP_U; ++u) c2[u] = (uint32_t)(bb + 64 * u);
+            for (int u = 0; u < U; ++u) c2[u] = (uint32_t)(bb + 64 * u);
             philox10_c2_multi(hd, c2, vk, o);
 #pragma unroll
-            for (int u = 0; u < FRAME_CAP_U; ++u) {
+            for (int u = 0; u < U; ++u) {
                 const Noise4 nz = noise4_of(o[u], Ksig);
                 v[u].x = fmaf(nz.r0, nz.c0, v[u].x); v[u].y = fmaf(nz.r0, nz.s0, v[u].y);
                 v[u].z = fmaf(nz.r1, nz.c1, v[u].z); v[u].w = fmaf(nz.r1, nz.s1, v[u].w);
@@ -612,7 +616,7 @@ __device__ __forceinline__ void capture_blocks(const A &a, int wave_len, float *
         }
         // samples of the block outside [0, L) land in the region's slack, never read as capture
 #pragma unroll
-        for (int u = 0; u < FRAME_CAP_U; ++u)
+        for (int u = 0; u < U; ++u)
             if (bb + 64 * u <= be) {
                 if constexpr (RING > 0) {
                     uint32_t pos = 4u * (uint32_t)(bb + 64 * u - b0);       // < 3 RING: two unsigned reductions
@@ -624,6 +628,58 @@ __device__ __forceinline__ void capture_blocks(const A &a, int wave_len, float *
                     *reinterpret_cast<float4 *>(rbase + 4 * (bb + 64 * u - b0)) = v[u];
                 }
             }
+    };
+    using U4 = std::integral_constant<int, FRAME_CAP_U>;
+    if constexpr (TRIM) {
+        int p0 = bs;
+        for (; be - p0 >= 3 * 64; p0 += FRAME_CAP_U * 64) pass(U4{}, p0);
+        if (be - p0 >= 2 * 64) pass(std::integral_constant<int, 3>{}, p0);
+        else if (be - p0 >= 64) pass(std::integral_constant<int, 2>{}, p0);
+        else if (be - p0 >= 0) pass(std::integral_constant<int, 1>{}, p0);
+    } else {
+        // whole passes, written out: the fixed kernel's max-ILP schedule is sensitive to the form (through `pass` it
+        // renames its registers and issues 10 instructions more)
+        for (int p0 = bs; p0 <= be; p0 += FRAME_CAP_U * 64) {
+            const int bb = p0 + lane;
+            float4 v[FRAME_CAP_U];
+#pragma unroll
+            for (int u = 0; u < FRAME_CAP_U; ++u) {
+                const int b = bb + 64 * u;
+                // the block's 4 clean real parts in one 16-B load (bm < pb: inside the table; the compiler keeps it under
+                // `in`, and forcing it on every lane measured 1 % slower, profiles/r04/ab/ab_ab_ntu.txt)
+                const float4 re = *reinterpret_cast<const float4 *>(a.wave_re + 4 * bm);
+                const bool in = (uint32_t)b < nb_wave;                     // past the waveform's end: zeros
+                v[u] = in ? re : make_float4(0.f, 0.f, 0.f, 0.f);
+                bm = bm + 64 >= pb ? bm + 64 - pb : bm + 64;           // (bm + 64) mod pb (pb > 64)
+            }
+            if (real) {         // sigma z = sqrt(K log2 u1) (cos | sin 2 pi u2) per pair
+                uint32_t c2[FRAME_CAP_U];
+                uint4 o[FRAME_CAP_U];
+#pragma unroll
+                for (int u = 0; u < FRAME_CAP_U; ++u) c2[u] = (uint32_t)(bb + 64 * u);
+                philox10_c2_multi(hd, c2, vk, o);
+#pragma unroll
+                for (int u = 0; u < FRAME_CAP_U; ++u) {
+                    const Noise4 nz = noise4_of(o[u], Ksig);
+                    v[u].x = fmaf(nz.r0, nz.c0, v[u].x); v[u].y = fmaf(nz.r0, nz.s0, v[u].y);
+                    v[u].z = fmaf(nz.r1, nz.c1, v[u].z); v[u].w = fmaf(nz.r1, nz.s1, v[u].w);
+                }
+            }
+            // samples of the block outside [0, L) land in the region's slack, never read as capture
+#pragma unroll
+            for (int u = 0; u < FRAME_CAP_U; ++u)
+                if (bb + 64 * u <= be) {
+                    if constexpr (RING > 0) {
+                        uint32_t pos = 4u * (uint32_t)(bb + 64 * u - b0);       // < 3 RING: two unsigned reductions
+                        pos = min(pos, pos - (uint32_t)RING);
+                        pos = min(pos, pos - (uint32_t)RING);
+                        *reinterpret_cast<float4 *>(rbase + pos) = v[u];
+                        if (pos < (uint32_t)EXT) *reinterpret_cast<float4 *>(rbase + pos + RING) = v[u];
+                    } else {
+                        *reinterpret_cast<float4 *>(rbase + 4 * (bb + 64 * u - b0)) = v[u];
+                    }
+                }
+        }
     }
 }
 
@@ -1435,9 +1491,9 @@ __global__ __launch_bounds__(64 * W, FRAME_LONG_MINW) void frame_sync_long_kerne
             return (int)min(x, x - (uint32_t)LW_RING);
         };
         // samples [n_lo, n_hi) into the ring (whole Philox blocks: up to 3 samples either side, with their own values)
-        auto gen = [&](int n_lo, int n_hi) {
-            capture_blocks<LW_RING, LW_EXT>(a, wave_len, rbase, b0, (rx_start + n_lo) >> 2, (rx_start + n_hi - 1) >> 2, lane,
-                                            t_lo, t_hi, qs, sigma);
+        auto gen = [&](int n_lo, int n_hi, auto trim) {
+            capture_blocks<LW_RING, LW_EXT, decltype(trim)::value>(a, wave_len, rbase, b0, (rx_start + n_lo) >> 2,
+                                                                  (rx_start + n_hi - 1) >> 2, lane, t_lo, t_hi, qs, sigma);
         };
         const int im0 = im_mod(rx_start);
         int lx = lane;
@@ -1510,7 +1566,7 @@ __global__ __launch_bounds__(64 * W, FRAME_LONG_MINW) void frame_sync_long_kerne
         };
         // round rho's piece: samples [rho LW_ROUND, min(L, rho LW_ROUND + LW_PIECE)), the ring then holding the last
         // LW_RING - 3 samples generated
-        auto piece = [&](int rho) { gen(rho * LW_ROUND, min(L, rho * LW_ROUND + LW_PIECE)); };
+        auto piece = [&](int rho) { gen(rho * LW_ROUND, min(L, rho * LW_ROUND + LW_PIECE), std::false_type{}); };
         piece(0);
         wave_lds_sync();
         detect(std::integral_constant<int, 0>{});
@@ -1569,17 +1625,20 @@ __global__ __launch_bounds__(64 * W, FRAME_LONG_MINW) void frame_sync_long_kerne
         }
         const bool sync_fail = cand == 0x7fffffff;
         const int p = sync_fail ? 0 : cand + 10 + 1;
-        // ---- the matched filter's samples [p - 20, p + 2 (nfr - 1) + 10] (at most 1,949 < LW_RING - 6): the ring holds
-        // [res_lo, res_hi) of them after the last round's piece; the missing end of the window is generated -- forward
-        // past res_hi (evicting only samples before the window) or backward below res_lo (evicting only samples past
-        // it).  A failed sync (p = 0) reads [0, 2 nfr - 10). ----
+        // ---- the matched filter's samples [p + 140, p + 2 (nfr - 1) + 10] (at most 1,789 < LW_RING - 6; the first
+        // instant read is frame sample 80, the STF's last 32 samples, whose window starts at p + 2 x 80 - 20): the ring
+        // holds [res_lo, res_hi) of them after the last round's piece; the missing end of the window is generated --
+        // forward past res_hi (evicting only samples before the window) or backward below res_lo (evicting only samples
+        // past it), its last capture pass only as many blocks per lane as it stores.  A failed sync (p = 0) reads
+        // [140, 2 nfr + 8]. ----
+        constexpr int MF_S_FIRST = 80;                        // the first run's first instant (the runs below)
         {
-            const int lo = max(p - 20, 0), hi = min(p + 2 * (nfr - 1) + 10, L - 1);
+            const int lo = p + 2 * MF_S_FIRST - 20, hi = min(p + 2 * (nfr - 1) + 10, L - 1);
             const int res_hi = min(L, held * LW_ROUND + LW_PIECE), res_lo = res_hi + 3 - LW_RING;
             if (hi >= res_hi || lo < res_lo) {
                 wave_lds_sync();                              // detection's loads are done
-                if (hi >= res_hi) gen(max(lo, res_hi), hi + 1);
-                else gen(lo, min(hi + 1, res_lo));
+                const bool fwd = hi >= res_hi;
+                gen(fwd ? max(lo, res_hi) : lo, fwd ? hi + 1 : min(hi + 1, res_lo), std::true_type{});
                 wave_lds_sync();
             }
         }
@@ -1609,7 +1668,7 @@ __global__ __launch_bounds__(64 * W, FRAME_LONG_MINW) void frame_sync_long_kerne
             int s0 = 0, e = 0;
             if (u < n_runs) {
                 if (u < c0r) {
-                    s0 = 80 + MF_RUN * u; e = 112;
+                    s0 = MF_S_FIRST + MF_RUN * u; e = 112;
                 } else if (u < c1r) {
                     s0 = 192 + MF_RUN * (u - c0r); e = 320;
                 } else {

@@ -76,20 +76,23 @@ def test_ring_reads_are_the_samples_meant(n_data):
             held = 2
         # a decided front lies below 2 LW_ROUND - 300; a failed sync gives p = 0
         p = 0 if rng.random() < 0.2 else int(rng.integers(11, (2 * LW_ROUND - 300) if decided else L - 60))
-        lo, hi = max(p - 20, 0), min(p + 2 * (nfr - 1) + 10, L - 1)
+        lo, hi = p + 2 * 80 - 20, min(p + 2 * (nfr - 1) + 10, L - 1)   # the first instant read is frame sample 80
         res_hi = min(L, held * LW_ROUND + LW_PIECE)
         res_lo = res_hi + 3 - LW_RING
         if hi >= res_hi:
             ring.gen(max(lo, res_hi), hi + 1)
         elif lo < res_lo:
             ring.gen(lo, min(hi + 1, res_lo))
-        # every matched-filter run in the capture reads 2 MF_RUN + 19 samples from ring(n_lo), n_lo = p + 2 s0 - 20
-        for s0 in range(0, nfr, MF_RUN):
+        # every matched-filter run (instants [80, 112), [192, 320), [336 + 80 d, 400 + 80 d) in runs of MF_RUN) in the
+        # capture reads 2 MF_RUN + 19 samples from ring(n_lo), n_lo = p + 2 s0 - 20
+        starts = [s for a, e in [(80, 112), (192, 320)] + [(336 + 80 * d, 400 + 80 * d) for d in range(n_data)]
+                  for s in range(a, e, MF_RUN)]
+        for s0 in starts:
             n_lo = p + 2 * s0 - 20
             if n_lo < 0 or p + 2 * (s0 + MF_RUN - 1) >= L:
                 continue                                          # the per-instant path (ring(mc) per sample)
             base = ring.at(n_lo)
             need = np.arange(n_lo, n_lo + 2 * MF_RUN + 19)
             assert np.array_equal(ring.f[base:base + len(need)], need), (p, s0)
-        for mc in (lo, hi, (lo + hi) // 2):                      # the per-instant path's single reads
+        for mc in ((lo, hi, (lo + hi) // 2) if lo <= hi else ()):  # the per-instant path's single reads
             assert ring.f[ring.at(mc)] == mc

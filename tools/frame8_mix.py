@@ -17,7 +17,8 @@ inlined call holding it (capture_blocks, the detect / select lambdas, ...), else
   * the per-instant matched-filter path (windows leaving the capture): 0, its per-pass skeleton 1/3 (pass 2's
     lanes past the 137 runs take it);
   * a capture call site's pass loop: piece(0), piece(1), piece(2) 2 passes per item (a round's 2,031 samples: <= 509
-    Philox blocks, 256 per pass), times the call site's weight; the window's missing end: the fixture's passes per item;
+    Philox blocks, 256 per pass), times the call site's weight; the window's missing end: the fixture's whole passes
+    per item (regen_full) in its loop, and its last pass of 3 / 2 / 1 blocks per lane at the fixture's rates;
   * the hand-off loop: 1 + n_data = 9 iterations;
   * every other instruction of the item loop: 1.
 g is the fraction tests/golden/frame8_path_rates.json records for the bench grid (a CPU simulation of the kernel's
@@ -154,13 +155,17 @@ def anchors() -> dict:
          "fb_inner_lo": src_line(t, "if (n >= L + 20) {", k),
          "handoff_lo": src_line(t, "for (int j = lx; j < 64 * nw; j += 64) {", k),
          "handoff_hi": src_line(t, "dst[win_off(n, a.ipb, nw) + w] = v;", k)}
-    a["regen_hi"] = src_line(t, "else gen(lo, min(hi + 1, res_lo));", a["regen_lo"] - 1)
+    a["regen_gen"] = src_line(t, "gen(fwd ? max(lo, res_hi) : lo, fwd ? hi + 1 : min(hi + 1, res_lo), std::true_type{});",
+                              a["regen_lo"] - 1)
+    a["regen_hi"] = a["regen_gen"] + 2
     a["fb_inner_hi"] = src_line(t, "v.y = fmaf(xi, h, v.y);", a["fb_inner_lo"] - 1)
     a["fb_hi"] = src_line(t, "mfo[pi][o] = v;", a["fb_inner_hi"] - 1)
     a["item_end"] = src_line(t, "// the next capture overwrites this item's region", a["handoff_hi"] - 1)
     a["undec_capture"] = src_line(t, "piece(2);", a["undec_lo"] - 1)
-    a["regen_fwd"] = src_line(t, "if (hi >= res_hi) gen(max(lo, res_hi), hi + 1);", a["regen_lo"] - 1)
-    a["regen_bwd"] = a["regen_hi"]
+    # capture_blocks<..., TRIM = true>'s last pass (the window's missing end): 3, 2 or 1 blocks per lane
+    cb = src_line(t, "__device__ __forceinline__ void capture_blocks(")
+    for u in (3, 2, 1):
+        a[f"tail{u}"] = src_line(t, f"pass(std::integral_constant<int, {u}>{{}}, p0);", cb)
     return a
 
 
@@ -211,10 +216,10 @@ def chains(ins, sites, rows) -> dict:
 
 def weights(ins, sites, rows, a, rates: dict, nw: int):
     """per-instruction weight as (constant, coefficient of u) -- the fixture's regeneration rates enter the constant:
-    items generating the end of their matched-filter window (forward) or its start (backward), and their passes"""
+    the items generating the missing end of their matched-filter window, their whole passes and their last pass's
+    width"""
     g = rates["regen"]
-    gf, gb = rates["regen_fwd"], rates["regen"] - rates["regen_fwd"]
-    pf, pb = rates["regen_fwd_passes"], rates["regen_passes"] - rates["regen_fwd_passes"]
+    tails = {u: rates[f"regen_tail{u}"] for u in (3, 2, 1)}
     ch = chains(ins, sites, rows)
     lp = loops(ins)
     item = max(lp, key=lambda l: l[1] - l[0])
@@ -234,26 +239,26 @@ def weights(ins, sites, rows, a, rates: dict, nw: int):
             w[addr] = (0.0, 0.0)
             continue
         c, cu = 1.0, 0.0
+        tail = None
         if within(c_, a["undec_lo"], a["undec_hi"] - 1):
             c, cu = 0.0, 1.0
-        elif within(c_, a["regen_fwd"], a["regen_fwd"]):
-            c = gf
-        elif within(c_, a["regen_bwd"], a["regen_bwd"]):
-            c = gb
         elif within(c_, a["regen_lo"], a["regen_hi"] + 1):
             c = g
+            tail = next((u for u in (3, 2, 1) if a[f"tail{u}"] in c_), None)
+            if tail is not None:                    # a last pass of `tail` blocks per lane: tails[tail] of the items
+                c = tails[tail]
         elif within(c_, a["fb_inner_lo"], a["fb_inner_hi"] + 2):
             c = 0.0
         elif within(c_, a["fb_lo"], a["fb_hi"]):
             c = 1.0 / 3.0
         mult = 1.0
-        if any(l[0] <= addr <= l[1] for l in phil):
-            sites_ = (a["piece0"], a["piece1"], a["undec_capture"], a["regen_fwd"], a["regen_bwd"])
+        if tail is None and any(l[0] <= addr <= l[1] for l in phil):
+            sites_ = (a["piece0"], a["piece1"], a["undec_capture"], a["regen_gen"])
             site = next((x for x in c_ if x in sites_), None)
-            # a round's piece: 2,031 samples, <= 509 Philox blocks = 2 passes of 256; the window's missing end: gp passes
-            # per item over the g items that generate it
-            mult = (1.0 if site is None else (pf / gf if gf else 0.0) if site == a["regen_fwd"]
-                    else (pb / gb if gb else 0.0) if site == a["regen_bwd"] else 2.0)
+            # a round's piece: 2,031 samples, <= 509 Philox blocks = 2 passes of 256; the window's missing end: its whole
+            # passes per item over the g items that generate it
+            mult = (1.0 if site is None else (rates["regen_full"] / g if g else 0.0) if site == a["regen_gen"]
+                    else 2.0)
         elif within(c_, a["handoff_lo"], a["handoff_hi"]) and any(l[0] <= addr <= l[1] for l in inner_loops):
             mult = float(nw)
         w[addr] = (c * mult, cu * mult)
