@@ -1423,8 +1423,9 @@ void launch_frame_fix(hipStream_t st, const FrameArgs &a, dim3 grid, size_t lds)
 //      only on earlier positions, and every later front lies past it.  Then round 2 and its samples are skipped;
 //      the rounds' crossing masks stay in registers, so the rule needs no samples;
 //   3. otherwise round 2's samples [3,968, L) -> round 2 and the selection over all three rounds (a.no_lazy: always);
-//   4. the matched filter's samples [p - 20, p + 2 (nfr - 1) + 10] (1,949 for 8 data symbols): the part the ring does
-//      not hold is generated (63 % of the bench's items, 0.88 capture passes per item on average).
+//   4. the samples the matched filter's runs read, [p + 140, p + 2 (nfr - 1) + 10] (1,789 for 8 data symbols): the
+//      part the ring does not hold is generated (57 % of the bench's items; 2.41 Philox blocks per lane and item on
+//      average, the last pass trimmed to the blocks it stores; profiles/r06/frame/ab_regen.txt).
 // Reads index the ring ((n + off) mod LW_RING): a lane's detection run (80 floats) and a matched-filter run (29) read
 // linearly through the mirror.  Round 6 A/Bs (profiles/r06/frame/ab_long12.txt, ab_ring.txt): two rounds resident
 // (16 KB per wave) in 9-wave blocks, 3, 2, 2, 2 waves on a CU's SIMDs 8.34-8.38e8; one round's piece in 12-wave blocks,

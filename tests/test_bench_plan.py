@@ -539,7 +539,7 @@ def test_frame8_classified_cap():
     sys.path.insert(0, str(ROOT / "tools"))
     import frame8_mix
     d = ROOT / "profiles" / "r06" / "pmc" / "frame8"
-    m = frame8_mix.model([d / "pmc_7", d / "pmc_2"], 32_000_000 / 8)          # 9-wave blocks: 3, 2, 2, 2 per SIMD
+    m = frame8_mix.model([d / "pmc_7", d / "pmc_2"], 32_000_000 / 8)          # 12-wave blocks: 3 waves on every SIMD
     assert abs(m["undecided_fraction"] - m["undecided_fraction_simulated"]) < 0.05
     assert abs(m["g_build_instr_delta"]) < 16
     assert 0.58 < m["sync"]["cap_frac"] < 0.71 and 0.55 < m["cap_frac"] < 0.75
