@@ -2,7 +2,8 @@
 every float a detection round or a matched-filter run reads must be the capture sample it means, for every capture
 offset, packet position and lazy outcome.  A ring slot here holds the sample index last written to it (the kernel
 writes whole Philox blocks of 4 samples at float 4 (b - b0) mod LW_RING, and blocks landing in [0, LW_EXT) also at
-their mirror past LW_RING)."""
+their mirror past LW_RING).  The matched-filter window's generation draws its blocks in trimmed passes, restated at the
+end."""
 import numpy as np
 import pytest
 
@@ -96,3 +97,35 @@ def test_ring_reads_are_the_samples_meant(n_data):
             assert np.array_equal(ring.f[base:base + len(need)], need), (p, s0)
         for mc in ((lo, hi, (lo + hi) // 2) if lo <= hi else ()):  # the per-instant path's single reads
             assert ring.f[ring.at(mc)] == mc
+
+
+def trimmed_passes(bs, be):
+    """capture_blocks<RING, EXT, TRIM = true>'s schedule (ofdm_frame.hip): (p0, U) per pass -- whole passes of 4 blocks
+    per lane while more than 192 blocks remain, then one pass of ceil(rest / 64) blocks per lane"""
+    out, p0 = [], bs
+    while be - p0 >= 3 * 64:
+        out.append((p0, 4))
+        p0 += 4 * 64
+    for u, need in ((3, 2 * 64), (2, 64), (1, 0)):
+        if be - p0 >= need:
+            out.append((p0, u))
+            break
+    return out
+
+
+def test_trimmed_passes_store_every_block_once():
+    """the matched-filter window's missing end (1..483 blocks): lane l of a pass (p0, U) stores blocks p0 + l + 64 u,
+    u < U, that are <= be -- together exactly [bs, be], each once, with ceil(n / 64) blocks per lane in all but whole
+    passes (n = be - bs + 1)"""
+    for n in range(1, 700):
+        bs = 17 + n
+        be = bs + n - 1
+        stored = []
+        lane_blocks = 0
+        for p0, u in trimmed_passes(bs, be):
+            lane_blocks += u
+            stored += [p0 + lane + 64 * k for k in range(u) for lane in range(64) if p0 + lane + 64 * k <= be]
+        assert sorted(stored) == list(range(bs, be + 1)), n
+        # whole passes for all but the last (n - 1) % 256 + 1 blocks, which take ceil(. / 64) blocks per lane
+        assert lane_blocks == 4 * ((n - 1) // 256) + -(-((n - 1) % 256 + 1) // 64), n
+        assert lane_blocks <= 4 * -(-n // 256), n                 # never more than whole passes
