@@ -32,14 +32,20 @@ CFLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-fno-slp-vecto
 # per-source flags: the symbol-mode kernels schedule for ILP (A/B: c3 +1 %, c2 +3 %, c5 +3 %; the
 # frame kernels -0.5 %, profiles/r01/ab/ab_*_ilp.json; packed receivers c3 +1.4 %, c2 +2.5 %,
 # profiles/r02/ab/SUMMARY.md).  The packed ideal-CSI receivers (ofdm_rxpack_ideal.hip) keep the default scheduler:
-# with the prologue's Tx builds, max-ILP spills them at their 168-VGPR budget.
+# with the prologue's Tx builds, max-ILP spills them at their 168-VGPR budget.  The fixed-geometry frame sync kernel
+# (ofdm_frame_fix.hip) schedules iterative-ILP and the long-capture kernel (ofdm_frame_long.hip) max-ILP (round 6,
+# interleaved: frame +0.9 % over max-ILP; frame8 +0.8 % over the default -- iterative-ILP +0.7 %, but the compiler
+# fails on that TU with -g, which tools/frame8_mix.py needs; the symbol kernel's TU is best at the default,
+# profiles/r06/frame/ab_sched.txt).
 SOURCE_FLAGS = {"ofdm_symbol.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
                 "ofdm_rxpack.hip": os.environ.get("OFDM_RXPACK_FLAGS", "-mllvm -amdgpu-sched-strategy=max-ilp").split(),
                 "ofdm_rxpack_ideal.hip": os.environ.get("OFDM_RXPACK_IDEAL_FLAGS", "").split(),
                 "ofdm_frame.hip": os.environ.get("OFDM_FRAME_FLAGS", "").split(),
                 "ofdm_frame_sym.hip": os.environ.get("OFDM_FRAME_SYM_FLAGS", "").split(),
-                "ofdm_frame_fix.hip": os.environ.get("OFDM_FRAME_FIX_FLAGS", "-mllvm -amdgpu-sched-strategy=max-ilp").split(),
-                "ofdm_frame_long.hip": os.environ.get("OFDM_FRAME_LONG_FLAGS", "").split()}
+                "ofdm_frame_fix.hip": os.environ.get("OFDM_FRAME_FIX_FLAGS",
+                                                     "-mllvm -amdgpu-sched-strategy=iterative-ilp").split(),
+                "ofdm_frame_long.hip": os.environ.get("OFDM_FRAME_LONG_FLAGS",
+                                                      "-mllvm -amdgpu-sched-strategy=max-ilp").split()}
 
 
 # Kernels whose parity-dump variants (last template argument `true`) are allowed to spill: they
