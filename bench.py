@@ -650,10 +650,13 @@ def main():
     sym_step = (PipelinedSymbolStep(torch, eng, cfg, chunks, counters, dev, fused=fused)
                 if not frame_mode and chunks else None)
 
+    frame_host = [None]           # frame mode's host counters of the last step (ofdm_frame_sweep returns them)
+
     def step():
         if frame_mode:            # one trial = one frame of dpf data symbols; waveform cached on the device
-            c = eng.frame_sweep(cfg, SNR_GRID, frames, first_trial=first)
-            counters.copy_(torch.from_numpy(c))
+            frame_host[0] = eng.frame_sweep(cfg, SNR_GRID, frames, first_trial=first)
+            if distributed:       # the all-reduce below works on the device tensor; one rank needs no device copy
+                counters.copy_(torch.from_numpy(frame_host[0]))
         elif sym_step is not None:
             sym_step()
         else:
@@ -683,6 +686,8 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev}")
         elapsed = host_allreduce(dist, t, dist.ReduceOp.MAX).item()
 
+    if frame_mode and not distributed:
+        counters.copy_(torch.from_numpy(frame_host[0]))
     c = counters.cpu().numpy()
     n_snr = len(SNR_GRID)
     job_frames = total_frames * (world if scaling == "weak" else 1)

@@ -133,6 +133,24 @@ int Ctx::ensure(void **p, size_t *cap, size_t bytes) {
     return OFDM_OK;
 }
 
+int Ctx::read_counters(void *out, size_t bytes) {
+    if (cap_h_cnt < bytes) {
+        if (h_cnt) hipHostFree(h_cnt);
+        h_cnt = nullptr;
+        cap_h_cnt = 0;
+        if (hipHostMalloc(&h_cnt, bytes, hipHostMallocDefault) != hipSuccess) {
+            h_cnt = nullptr;
+            return set_error(OFDM_E_NOMEM, "hipHostMalloc(%zu) failed", bytes);
+        }
+        cap_h_cnt = bytes;
+    }
+    hipError_t e = hipMemcpyAsync(h_cnt, d_cnt, bytes, hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    if (e != hipSuccess) return set_error(OFDM_E_HIP, "counter read-back: %s", hipGetErrorString(e));
+    std::memcpy(out, h_cnt, bytes);
+    return OFDM_OK;
+}
+
 }  // namespace ofdm
 
 #define HIPOK(expr)                                                                             \
@@ -209,6 +227,7 @@ int ofdm_ctx_destroy(ofdm_ctx *ctx) {
         if (p) hipFree(p);
     for (hipEvent_t ev : {c->ev_start, c->ev_tx[0], c->ev_tx[1], c->ev_rx[0], c->ev_rx[1]})
         if (ev) hipEventDestroy(ev);
+    if (c->h_cnt) hipHostFree(c->h_cnt);
     if (c->tx_stream) hipStreamDestroy(c->tx_stream);
     if (c->own) hipStreamDestroy(c->own);
     delete c;
@@ -564,9 +583,7 @@ int ofdm_symbol_sweep(ofdm_ctx *ctx, const ofdm_cfg *cfg, const double *snr_db, 
                         : ofdm_rx_frames(ctx, cfg, txbuf[k & 1], bitbuf[k & 1], fk, nk, snr_db, n_snr, c->d_cnt);
             if (rc) return rc;
         }
-        HIPOK(hipMemcpyAsync(counters, c->d_cnt, cbytes, hipMemcpyDeviceToHost, c->stream));
-        HIPOK(hipStreamSynchronize(c->stream));
-        return OFDM_OK;
+        return c->read_counters(counters, cbytes);
     }
     if ((rc = ofdm_tx_frames(ctx, cfg, f0, n0, txbuf[0], bitbuf[0]))) return rc;
     for (int64_t k = 0; k < n_chunks; ++k) {
@@ -586,9 +603,7 @@ int ofdm_symbol_sweep(ofdm_ctx *ctx, const ofdm_cfg *cfg, const double *snr_db, 
         if ((rc = ofdm_rx_frames(ctx, cfg, txbuf[k & 1], bitbuf[k & 1], fk, nk, snr_db, n_snr, c->d_cnt))) return rc;
         if (n_chunks > 1) HIPOK(hipEventRecord(c->ev_rx[k & 1], main_stream));
     }
-    HIPOK(hipMemcpyAsync(counters, c->d_cnt, cbytes, hipMemcpyDeviceToHost, c->stream));
-    HIPOK(hipStreamSynchronize(c->stream));
-    return OFDM_OK;
+    return c->read_counters(counters, cbytes);
 }
 
 }  // extern "C"

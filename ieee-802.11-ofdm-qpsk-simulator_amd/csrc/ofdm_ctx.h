@@ -41,6 +41,10 @@ struct Ctx {
     hipEvent_t ev_start = nullptr, ev_tx[2] = {nullptr, nullptr}, ev_rx[2] = {nullptr, nullptr};
     void *d_wave = nullptr;
     void *d_work = nullptr;          // K3c's work-item counter (one receiver launch in flight per context)
+    // pinned host staging for the sweeps' counter read-back (a pageable destination costs HIP a staging copy kernel
+    // and a host round trip per call); grown on demand, freed with the context
+    void *h_cnt = nullptr;
+    size_t cap_h_cnt = 0;
     size_t cap_tx = 0, cap_bits = 0, cap_cnt = 0, cap_scratch = 0, cap_scratch2 = 0, cap_wave = 0;
     // frame-mode waveform cache (per conv/payload/message)
     int wave_key = -1;
@@ -59,6 +63,8 @@ struct Ctx {
     void toc();
     void resolve();
     int ensure(void **p, size_t *cap, size_t bytes);
+    // d_cnt[0, bytes) -> host `out` on `stream` through the pinned staging buffer; returns after the copy has landed
+    int read_counters(void *out, size_t bytes);
 };
 
 }  // namespace ofdm

@@ -2111,13 +2111,16 @@ int ofdm_frame_sweep(ofdm_ctx *ctx, const ofdm_cfg *cfg, const ofdm_rx_opts *opt
     const size_t cbytes = (size_t)n_snr * OFDM_NCOUNTERS * 8;
     const size_t pbytes = packet_idx ? (size_t)n_snr * n_trials * 4 : 0;
     if ((rc = c->ensure(&c->d_cnt, &c->cap_cnt, cbytes + pbytes + 256))) return rc;
-    std::vector<int64_t> init((size_t)n_snr * OFDM_NCOUNTERS, 0);
-    if (opts->word_stats)
+    if (opts->word_stats) {                       // the word-length extremes start at +/- infinity
+        std::vector<int64_t> init((size_t)n_snr * OFDM_NCOUNTERS, 0);
         for (int q = 0; q < n_snr; ++q) {
             init[(size_t)q * OFDM_NCOUNTERS + OFDM_C_WL_MIN_Q] = INT64_MAX;
             init[(size_t)q * OFDM_NCOUNTERS + OFDM_C_WL_MAX_Q] = INT64_MIN;
         }
-    HIPOK(hipMemcpyAsync(c->d_cnt, init.data(), cbytes, hipMemcpyHostToDevice, c->stream));
+        HIPOK(hipMemcpyAsync(c->d_cnt, init.data(), cbytes, hipMemcpyHostToDevice, c->stream));
+    } else {
+        HIPOK(hipMemsetAsync(c->d_cnt, 0, cbytes, c->stream));
+    }
     int32_t *dp = packet_idx ? (int32_t *)((char *)c->d_cnt + ((cbytes + 255) & ~size_t(255))) : nullptr;
     for (int q0 = 0; q0 < n_snr; q0 += OFDM_MAX_SNR) {
         FrameArgs a{};
@@ -2167,9 +2170,8 @@ int ofdm_frame_sweep(ofdm_ctx *ctx, const ofdm_cfg *cfg, const ofdm_rx_opts *opt
                     (double)hs[k] / (double)(n_trials * a.n_snr));
 #endif
     }
-    HIPOK(hipMemcpyAsync(counters, c->d_cnt, cbytes, hipMemcpyDeviceToHost, c->stream));
     if (dp) HIPOK(hipMemcpyAsync(packet_idx, dp, pbytes, hipMemcpyDeviceToHost, c->stream));
-    HIPOK(hipStreamSynchronize(c->stream));
+    if ((rc = c->read_counters(counters, cbytes))) return rc;     // pinned staging; returns once the copies landed
     if (opts->word_stats && n_trials > 0)
         for (int q = 0; q < n_snr; ++q) {
             int64_t *row = counters + (size_t)q * OFDM_NCOUNTERS;
