@@ -1908,14 +1908,14 @@ static int32_t word_bits(double mn, double mx) {
     return max_abs < 1.0f ? 1 : (int32_t)std::ceil(std::log2((double)max_abs)) + 1;
 }
 
-// items per sync -> symbol hand-off: 2^22 items x 2 KB (reference message) = 8 GB of HBM, one launch pair per
-// 4M items (A/B, frame mode: 2^18 3.13e8, 2^20 3.33e8, 2^22 3.40e8 symbol-SNR/s -- each pair ends in a tail
-// and K4b' waits for K4b)
-#define FRAME_CHUNK_LOG2 22
+// items per sync -> symbol hand-off: 2^23 items x 1.5 KB (reference message) = 12 GiB of HBM, one launch pair per
+// 8M items (A/B, frame mode: 2^18 3.13e8, 2^20 3.33e8, 2^22 3.40e8 symbol-SNR/s; round 6, 2^23 over 2^22: frame
+// +0.4 %, frame8 +0.4 %, profiles/r06/frame/ab_chunk.txt -- each pair ends in a tail and K4b' waits for K4b)
+#define FRAME_CHUNK_LOG2 23
 constexpr int64_t FRAME_CHUNK_ITEMS = int64_t(1) << FRAME_CHUNK_LOG2;
-// items per chunk for n_data data symbols: 2^22, capped so that the hand-off buffer holds no more windows than the
-// reference message's 2^22 items do (1 + n_data windows of 512 B per item: 6 GiB; ADVICE r3: 8-symbol messages
-// would otherwise take 19 GiB)
+// items per chunk for n_data data symbols: 2^23, capped so that the hand-off buffer holds no more windows than the
+// reference message's 2^23 items do (1 + n_data windows of 512 B per item: 12 GiB; ADVICE r3: 8-symbol messages
+// would otherwise take 38 GiB)
 static int64_t frame_chunk_items(int n_data) {
     return std::min<int64_t>(FRAME_CHUNK_ITEMS, FRAME_CHUNK_ITEMS * 3 / (1 + n_data));
 }

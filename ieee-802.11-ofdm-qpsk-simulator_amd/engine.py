@@ -70,7 +70,7 @@ class Engine:
         check(self.lib, self.lib.ofdm_ctx_synchronize(self.ctx), "synchronize")
 
     def trim(self) -> int:
-        """Free the context's sweep scratch (ofdm_ctx_trim: up to 6 GiB of frame-sweep hand-off buffer); returns
+        """Free the context's sweep scratch (ofdm_ctx_trim: up to 12 GiB of frame-sweep hand-off buffer); returns
         the bytes released.  Later sweeps allocate it again."""
         n = C.c_int64()
         check(self.lib, self.lib.ofdm_ctx_trim(self.ctx, C.byref(n)), "ctx_trim")

@@ -104,7 +104,7 @@ int ofdm_ctx_destroy(ofdm_ctx *ctx);
 int ofdm_ctx_set_stream(ofdm_ctx *ctx, void *hip_stream);
 int ofdm_ctx_synchronize(ofdm_ctx *ctx);
 /* Release the context's sweep scratch (Tx batches of ofdm_symbol_sweep, the frame sweep's sync -> symbol
- * hand-off buffer of up to 6 GiB, counters, capture staging) after waiting for the context's streams; the
+ * hand-off buffer of up to 12 GiB, counters, capture staging) after waiting for the context's streams; the
  * waveform cache and LTF tables stay.  Later calls grow the scratch again on demand.  `released` (optional)
  * receives the bytes freed.  (The reference holds no device memory; its buffers are stack/heap arrays freed
  * when Receiver() returns, OFDM.c:941-1165.) */

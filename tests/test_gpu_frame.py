@@ -254,7 +254,7 @@ def test_frame_sweep_two_chunks_equal_their_halves(engine, pkg):
     chunk each)."""
     cfg = pkg.make_cfg(payload="message")
     snrs = np.arange(0.0, 31.0, 2.0)
-    n = 300_000                                   # 4.8M items: two chunks
+    n = 600_000                                   # 9.6M items: two chunks of at most 2^23
     whole, wp = engine.frame_sweep(cfg, snrs, n, want_packet_idx=True)
     a, ap = engine.frame_sweep(cfg, snrs, n // 2, want_packet_idx=True)
     b, bp = engine.frame_sweep(cfg, snrs, n // 2, first_trial=n // 2, want_packet_idx=True)
@@ -264,7 +264,7 @@ def test_frame_sweep_two_chunks_equal_their_halves(engine, pkg):
 
 def _halved_chunk(nd, cap_items):
     """the chunk ofdm_frame_sweep ends up with (ofdm_frame.hip frame_chunk_items + the NOMEM halving loop)"""
-    chunk = min(1 << 22, (1 << 22) * 3 // (1 + nd))
+    chunk = min(1 << 23, (1 << 23) * 3 // (1 + nd))
     while chunk > cap_items and chunk > (1 << 16):
         chunk //= 2
     return chunk
